@@ -1,0 +1,310 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE
+(/root/reference, read-only) in the build container.
+
+Run:  python tests/golden/make_golden.py     (needs /root/reference; CPU only)
+
+The reference's third-party imports that are absent offline are replaced by
+minimal stand-ins installed into sys.modules before import:
+  * timm.models.layers: DropPath (identity; all goldens use drop_path=0),
+    to_2tuple, trunc_normal_   (swinv2.py:9)
+  * composer.metrics.CrossEntropy, torchmetrics.Metric,
+    torchvision.datasets.ImageFolder  (hierarchy.py:6-15; only used as base
+    classes -- none of the functions exercised here touch them)
+Every array written is data (inputs and the reference's outputs); no reference
+source is copied into the repo.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.environ.get("HV_REFERENCE", "/root/reference")
+
+
+def install_shims():
+    timm = types.ModuleType("timm")
+    tm = types.ModuleType("timm.models")
+    tml = types.ModuleType("timm.models.layers")
+
+    class DropPath(torch.nn.Module):
+        def __init__(self, p=0.0):
+            super().__init__()
+            self.p = p
+
+        def forward(self, x):
+            assert not self.training or self.p == 0.0
+            return x
+
+    tml.DropPath = DropPath
+    tml.to_2tuple = lambda x: tuple(x) if isinstance(x, (list, tuple)) else (x, x)
+    tml.trunc_normal_ = lambda t, std=1.0, **k: torch.nn.init.trunc_normal_(t, std=std)
+    sys.modules.update({"timm": timm, "timm.models": tm, "timm.models.layers": tml})
+
+    composer = types.ModuleType("composer")
+    cm = types.ModuleType("composer.metrics")
+
+    class CrossEntropy:  # placeholder base class
+        pass
+
+    cm.CrossEntropy = CrossEntropy
+    composer.metrics = cm
+    sys.modules.update({"composer": composer, "composer.metrics": cm})
+
+    tmx = types.ModuleType("torchmetrics")
+
+    class Metric(torch.nn.Module):
+        pass
+
+    tmx.Metric = Metric
+    sys.modules["torchmetrics"] = tmx
+    tv = types.ModuleType("torchvision")
+    tvd = types.ModuleType("torchvision.datasets")
+
+    class ImageFolder:
+        pass
+
+    tvd.ImageFolder = ImageFolder
+    tv.datasets = tvd
+    sys.modules.update({"torchvision": tv, "torchvision.datasets": tvd})
+
+
+def main():
+    install_shims()
+    sys.path.insert(0, REF)
+    sys.path.insert(0, REPO)
+    import hierarchy as ref_h  # noqa: E402  (reference)
+    import swinv2 as ref  # noqa: E402  (reference)
+    from oracle.hierarchy_ref import synthetic_inat_names
+    from oracle.swinv2_ref import init_params_from_rng
+
+    torch.manual_seed(0)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+    # ---------------------------------------------------------------- indices
+    idx = {}
+    for w, pws in [(7, [0, 12]), (8, [0]), (12, [0, 12]), (24, [0, 12, 6]), (6, [0])]:
+        for pw in pws:
+            wa = ref.WindowAttention(dim=32, window_size=(w, w), num_heads=1,
+                                     pretrained_window_size=(pw, pw))
+            idx[f"rpi_w{w}"] = wa.relative_position_index.numpy()
+            idx[f"coords_w{w}_pw{pw}"] = wa.relative_coords_table.numpy()
+    for res, w, s in [(56, 7, 3), (28, 7, 3), (14, 7, 3), (7, 7, 3), (56, 7, 0),
+                      (96, 24, 12), (48, 24, 12), (24, 24, 12), (12, 24, 12),
+                      (64, 8, 4), (16, 8, 4)]:
+        blk = ref.SwinTransformerBlock(dim=32, input_resolution=(res, res), num_heads=1,
+                                       window_size=w, shift_size=s)
+        ew, es = blk.window_size, blk.shift_size
+        key = f"r{res}_w{w}_s{s}"
+        idx[key + "_eff"] = np.array([ew, es], np.int64)
+        idx[key + "_mask"] = (blk.attn_mask.numpy() if blk.attn_mask is not None
+                              else np.zeros((0,), np.float32))
+        img = torch.arange(res * res, dtype=torch.float64).reshape(1, res, res, 1)
+        if es > 0:
+            img = torch.roll(img, shifts=(-es, -es), dims=(1, 2))
+        win = ref.window_partition(img, ew).reshape(-1, ew * ew)
+        idx[key + "_gather"] = win.numpy().astype(np.int32)
+    for res in [56, 28, 14, 96, 48, 24]:
+        pm = ref.PatchMerging((res, res), dim=1)
+        pm.reduction = torch.nn.Identity()
+        pm.norm = torch.nn.Identity()
+        x = torch.arange(res * res, dtype=torch.float64).reshape(1, res * res, 1)
+        idx[f"merge_r{res}"] = pm(x)[0].numpy().astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "index_golden.npz"), **idx)
+
+    # ---------------------------------------------------------------- modules
+    mods = {}
+
+    def set_params(m, seed):
+        shapes = {k: v.shape for k, v in m.state_dict().items()
+                  if v.dtype.is_floating_point and not k.endswith("logit_clamp_max")
+                  and "relative_coords_table" not in k and "attn_mask" not in k}
+        p = init_params_from_rng(shapes, seed)
+        m.load_state_dict(p, strict=False)
+        return p
+
+    def run(m, prefix, x, seed, mask=None):
+        x = x.clone().requires_grad_(True)
+        y = m(x) if mask is None else m(x, mask=mask)
+        g = torch.from_numpy(np.random.default_rng(seed + 1).standard_normal(
+            tuple(y.shape)).astype(np.float32))
+        y.backward(g)
+        mods[prefix + "x"] = x.detach().numpy()
+        mods[prefix + "y"] = y.detach().numpy()
+        mods[prefix + "gy"] = g.numpy()
+        mods[prefix + "gx"] = x.grad.numpy()
+        for k, v in m.named_parameters():
+            if v.grad is not None:
+                mods[prefix + "grad." + k] = v.grad.numpy()
+
+    rng = np.random.default_rng(1234)
+    # WindowAttention with a shift mask: dim 64, 2 heads (head_dim 32), w 7, res 14
+    blk = ref.SwinTransformerBlock(dim=64, input_resolution=(14, 14), num_heads=2,
+                                   window_size=7, shift_size=3)
+    wa = blk.attn
+    set_params(wa, 11)
+    xw = torch.from_numpy(rng.standard_normal((2 * 4, 49, 64)).astype(np.float32))
+    run(wa, "wattn_mask.", xw, 12, mask=blk.attn_mask)
+    set_params(wa, 13)
+    run(wa, "wattn_nomask.", xw, 14)
+    for s in (0, 3):
+        blk = ref.SwinTransformerBlock(dim=64, input_resolution=(14, 14), num_heads=2,
+                                       window_size=7, shift_size=s)
+        set_params(blk, 20 + s)
+        x = torch.from_numpy(rng.standard_normal((2, 196, 64)).astype(np.float32))
+        run(blk, f"block_s{s}.", x, 30 + s)
+    # 16x16 map, window 8 (N = 64), shifted
+    blk = ref.SwinTransformerBlock(dim=64, input_resolution=(16, 16), num_heads=2,
+                                   window_size=8, shift_size=4)
+    set_params(blk, 40)
+    x = torch.from_numpy(rng.standard_normal((2, 256, 64)).astype(np.float32))
+    run(blk, "block_w8s4.", x, 41)
+    pm = ref.PatchMerging((14, 14), dim=32)
+    set_params(pm, 50)
+    x = torch.from_numpy(rng.standard_normal((2, 196, 32)).astype(np.float32))
+    run(pm, "merge.", x, 51)
+    mlp = ref.Mlp(in_features=32, hidden_features=128)
+    set_params(mlp, 60)
+    x = torch.from_numpy(rng.standard_normal((3, 5, 32)).astype(np.float32))
+    run(mlp, "mlp.", x, 61)
+    np.savez_compressed(os.path.join(HERE, "module_golden.npz"), **mods)
+
+    # ---------------------------------------------------------------- models
+    models = {}
+    cfgs = {
+        # tiny config for fast tests: stage0 res 14 (shifted 2x2 windows), stage1 7x7
+        "mini": dict(img_size=56, embed_dim=32, depths=[2, 2], num_heads=[1, 2],
+                     window_size=7, num_classes=10, drop_path_rate=0.0),
+        "mini_mt": dict(img_size=56, embed_dim=32, depths=[2, 2], num_heads=[1, 2],
+                        window_size=7, num_classes=(3, 4, 5, 6, 7, 8, 9),
+                        drop_path_rate=0.0),
+        "tiny": dict(img_size=224, embed_dim=96, depths=[2, 2, 6, 2],
+                     num_heads=[3, 6, 12, 24], window_size=7, num_classes=1000,
+                     drop_path_rate=0.0),
+    }
+    for name, cfg in cfgs.items():
+        net = ref.SwinTransformerV2(**cfg).eval()
+        shapes = {k: v.shape for k, v in net.state_dict().items()
+                  if k.endswith(("weight", "bias", "logit_scale"))
+                  and "relative" not in k}
+        p = init_params_from_rng(shapes, 7)
+        missing, unexpected = net.load_state_dict(p, strict=False)
+        assert not unexpected, unexpected
+        b = 2
+        x = torch.from_numpy(np.random.default_rng(42).standard_normal(
+            (b, 3, cfg["img_size"], cfg["img_size"])).astype(np.float32))
+        with torch.no_grad():
+            y = net(x)
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                yb = net(x)
+        if isinstance(y, list):
+            for i, (a, c) in enumerate(zip(y, yb)):
+                models[f"{name}.logits{i}"] = a.numpy()
+                models[f"{name}.logits_bf16_{i}"] = c.float().numpy()
+        else:
+            models[f"{name}.logits"] = y.numpy()
+            models[f"{name}.logits_bf16"] = yb.float().numpy()
+        models[f"{name}.n_state_keys"] = np.array(len(net.state_dict()))
+        models[f"{name}.macs"] = np.array(net.flops(), np.float64)
+        if name == "mini":
+            # one backward for the parameter-gradient parity test
+            net.train()
+            xx = x.clone().requires_grad_(True)
+            out = net(xx)
+            g = torch.from_numpy(np.random.default_rng(43).standard_normal(
+                tuple(out.shape)).astype(np.float32))
+            out.backward(g)
+            models["mini.gx"] = xx.grad.numpy()
+            for k, v in net.named_parameters():
+                models["mini.grad." + k] = v.grad.numpy()
+    keys = list(ref.SwinTransformerV2(**cfgs["tiny"]).state_dict().keys())
+    models["tiny.state_keys"] = np.array(keys)
+    np.savez_compressed(os.path.join(HERE, "model_golden.npz"), **models)
+
+    # ---------------------------------------------------------------- taxonomy
+    tax = {}
+    names = synthetic_inat_names()
+    rng = np.random.default_rng(5)
+    shuffled = list(rng.permutation(np.array(names)))
+    classes, c2i = ref_h.HierarchicalImageFolder.find_classes(
+        types.SimpleNamespace(), _FakeDir(shuffled))
+    tax["synthetic.classes"] = np.array(classes)
+    tax["synthetic.ids"] = np.stack([c2i[c].numpy() for c in classes]).astype(np.int64)
+    nc = tuple(int(tax["synthetic.ids"][:, t].max()) + 1 for t in range(7))
+    tax["synthetic.num_classes"] = np.array(nc)
+    hand = ["00001_animalia_chordata_aves_accipitriformes_accipitridae_haliaeetus_leucocephalus",
+            "00002_animalia_chordata_reptilia_accipitriformes_accipitridae_haliaeetus_leucocephalus",
+            "00000_plantae_tracheophyta_magnoliopsida_rosales_rosaceae_rosa_canina",
+            "00003_plantae_tracheophyta_magnoliopsida_rosales_rosaceae_rosa_rugosa",
+            "00004_fungi_basidiomycota_agaricomycetes_agaricales_amanitaceae_amanita_muscaria"]
+    classes, c2i = ref_h.HierarchicalImageFolder.find_classes(
+        types.SimpleNamespace(), _FakeDir(hand))
+    tax["hand.classes"] = np.array(classes)
+    tax["hand.ids"] = np.stack([c2i[c].numpy() for c in classes]).astype(np.int64)
+    tax["hand.tiers"] = np.array([ref_h.HierarchicalLabel.parse(c).clean_tiers for c in classes])
+    labels = [ref_h.HierarchicalLabel.parse(c) for c in classes]
+    tax["hand.dist"] = np.array([[a.dist(b) for b in labels] for a in labels], np.int64)
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        for split in ("train", "val"):
+            os.makedirs(os.path.join(d, split))
+        sub = names[:: 97]
+        for i, n in enumerate(sub):
+            os.makedirs(os.path.join(d, "train" if i % 3 else "val", n))
+        vecs = ref_h.build_parent_label_lookup(d)
+        tax["parent.names"] = np.array(sub)
+        for i, v in enumerate(vecs):
+            tax[f"parent.vec{i}"] = v
+    np.savez_compressed(os.path.join(HERE, "taxonomy_golden.npz"), **tax)
+
+    # ---------------------------------------------------------------- losses
+    loss = {}
+    sizes = (3, 13, 51, 273, 1103, 4884, 10000)
+    coeffs = [8, 5.65, 4, 2.82, 2, 1.41, 1]
+    rng = np.random.default_rng(77)
+    b = 4
+    logits = [torch.from_numpy((2.0 * rng.standard_normal((b, n))).astype(np.float32))
+              for n in sizes]
+    targets = torch.from_numpy(np.stack([rng.integers(0, n, b) for n in sizes], 1))
+    fn = ref_h.MultitaskCrossEntropy(coeffs=coeffs)
+    lh = fn(logits, targets)
+    eps = 0.08
+    soft = [torch.nn.functional.one_hot(t, n).float() * (1 - eps) + eps / n
+            for t, n in zip(targets.T, sizes)]
+    ls = fn(logits, soft)
+    for i, z in enumerate(logits):
+        loss[f"mt.logits{i}"] = z.numpy()
+    loss["mt.targets"] = targets.numpy()
+    loss["mt.coeffs"] = np.array(coeffs, np.float32)
+    loss["mt.loss_hard"] = np.array(float(lh))
+    loss["mt.loss_soft"] = np.array(float(ls))
+    loss["mt.smoothing"] = np.array(eps)
+    np.savez_compressed(os.path.join(HERE, "loss_golden.npz"), **loss)
+    print("goldens written to", HERE)
+
+
+class _FakeDir(str):
+    """find_classes() scans a directory; hand it names through os.scandir."""
+
+    def __new__(cls, names):
+        s = super().__new__(cls, "<fake>")
+        s.names = list(names)
+        return s
+
+
+_real_scandir = os.scandir
+
+
+def _scandir(path="."):
+    if isinstance(path, _FakeDir):
+        return iter([types.SimpleNamespace(name=n, is_dir=lambda: True) for n in path.names])
+    return _real_scandir(path)
+
+
+os.scandir = _scandir
+
+if __name__ == "__main__":
+    main()
