@@ -1,0 +1,80 @@
+"""ctypes binding of libhvk.so (C ABI declared in include/hvk.h).
+
+The product path has exactly one implementation of every hot op: the HIP
+kernels in this library.  There is no CPU or eager fallback -- if the library
+is missing or a tensor is not on the GPU the call raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  -- must be imported first: libhvk binds to torch's HIP runtime
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhvk.so")
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); kept in the order of include/hvk.h
+SIGNATURES = {
+    "hvk_abi_version": (_i, []),
+    "hvk_last_error_string": (ctypes.c_char_p, []),
+    "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
+    "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),
+    "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
+                                 _sz, _p]),
+    "hvk_patch_merge_gather": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "hvk_patch_merge_scatter": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "hvk_multitask_ce_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
+    "hvk_multitask_ce_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "hvk_hxe_fwd": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "hvk_hxe_bwd": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libhvk.so once and attach the signatures of include/hvk.h."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (or `make -C hierarchical-vision_amd/csrc`).  There is no fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    """Invoke an hvk_* entry point and raise RuntimeError on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.hvk_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"{name} failed (status {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Refuses CPU tensors."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("libhvk ops run on the GPU only; got a CPU tensor")
+    if not t.is_contiguous():
+        raise RuntimeError("libhvk ops need contiguous tensors")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)

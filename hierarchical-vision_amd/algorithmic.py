@@ -1,0 +1,152 @@
+"""Composer-style algorithms that touch the hot path (algorithmic.py).
+
+Minimal Event / State / Algorithm surface (match(event, state) / apply(event,
+state, logger)) so the reference's `algorithms:` YAML entries drive this
+trainer the way they drive composer.Trainer (main.py:98-102).
+"""
+import enum
+import math
+
+import torch
+
+
+class Event(enum.Enum):
+    INIT = "init"
+    BATCH_START = "batch_start"
+    BEFORE_FORWARD = "before_forward"
+    AFTER_FORWARD = "after_forward"
+    BEFORE_LOSS = "before_loss"
+    AFTER_LOSS = "after_loss"
+    BEFORE_BACKWARD = "before_backward"
+    AFTER_BACKWARD = "after_backward"
+    BATCH_END = "batch_end"
+
+
+class State:
+    """The slice of composer.State the algorithms use."""
+
+    def __init__(self, model, optimizer=None):
+        self.model = model
+        self.optimizers = [optimizer] if optimizer is not None else []
+        self.batch = None
+        self.outputs = None
+        self.loss = None
+        self.timestamp_batch = 0
+
+    def batch_get_item(self, key):
+        return self.batch[key]
+
+    def batch_set_item(self, key, value):
+        b = list(self.batch)
+        b[key] = value
+        self.batch = tuple(b)
+
+
+class Algorithm:
+    def match(self, event, state) -> bool:
+        raise NotImplementedError
+
+    def apply(self, event, state, logger=None):
+        raise NotImplementedError
+
+
+def smooth_labels(logits: torch.Tensor, target: torch.Tensor, smoothing: float = 0.1):
+    """(one_hot(target) * (1 - smoothing)) + smoothing / n_classes (algorithmic.py:160-164)."""
+    n_classes = logits.shape[1]
+    if target.dtype.is_floating_point and target.shape == logits.shape:
+        one_hot = target
+    else:
+        one_hot = torch.nn.functional.one_hot(target.long(), n_classes).to(logits.dtype)
+    return (one_hot.float() * (1.0 - smoothing)) + (smoothing / n_classes)
+
+
+class LabelSmoothing(Algorithm):
+    """Label smoothing that also handles multitask list outputs (algorithmic.py:88-119):
+    BEFORE_LOSS swaps the targets for smoothed probability targets (one per tier
+    for list outputs); AFTER_LOSS restores the originals."""
+
+    def __init__(self, smoothing=0.1, target_key=1):
+        self.smoothing = smoothing
+        self.target_key = target_key
+        self.original_labels = None
+
+    def match(self, event, state):
+        return event in (Event.BEFORE_LOSS, Event.AFTER_LOSS)
+
+    def apply(self, event, state, logger=None):
+        if event == Event.BEFORE_LOSS:
+            labels = state.batch_get_item(self.target_key)
+            assert isinstance(labels, torch.Tensor), "type error"
+            self.original_labels = labels.clone()
+            if isinstance(state.outputs, list):
+                b, tiers = labels.shape
+                assert len(state.outputs) == tiers, "different level of tiers"
+                assert all(o.shape[0] == b for o in state.outputs), "different batch sizes"
+                smoothed = [smooth_labels(o, t, self.smoothing) for o, t in zip(state.outputs, labels.T)]
+            else:
+                smoothed = smooth_labels(state.outputs, labels, self.smoothing)
+            state.batch_set_item(self.target_key, smoothed)
+        elif event == Event.AFTER_LOSS:
+            state.batch_set_item(self.target_key, self.original_labels)
+
+
+class GradientClipping(Algorithm):
+    """Global-norm (or value) clipping after backward (configs/pretrain/inat21.yaml:44-47)."""
+
+    def __init__(self, clipping_type="norm", clipping_threshold=2.0):
+        if clipping_type not in ("norm", "value"):
+            raise ValueError(clipping_type)
+        self.clipping_type = clipping_type
+        self.clipping_threshold = clipping_threshold
+
+    def match(self, event, state):
+        return event == Event.AFTER_BACKWARD
+
+    def apply(self, event, state, logger=None):
+        params = [p for p in state.model.parameters() if p.grad is not None]
+        if self.clipping_type == "norm":
+            torch.nn.utils.clip_grad_norm_(params, self.clipping_threshold, foreach=True)
+        else:
+            torch.nn.utils.clip_grad_value_(params, self.clipping_threshold, foreach=True)
+
+
+class EMA(Algorithm):
+    """Exponential moving average of the weights every `update_interval` batches with
+    smoothing from a half-life in batches (configs/pretrain/inat21.yaml:32-35)."""
+
+    def __init__(self, half_life="100ba", update_interval="20ba", smoothing=None):
+        hl = int(str(half_life).rstrip("ba"))
+        self.update_interval = int(str(update_interval).rstrip("ba"))
+        self.smoothing = smoothing if smoothing is not None else math.exp(
+            -math.log(2) * self.update_interval / hl)
+        self.ema_params = None
+
+    def match(self, event, state):
+        return event == Event.BATCH_END
+
+    @torch.no_grad()
+    def apply(self, event, state, logger=None):
+        params = [p for p in state.model.parameters()]
+        if self.ema_params is None:
+            self.ema_params = [p.detach().clone() for p in params]
+            return
+        if state.timestamp_batch % self.update_interval:
+            return
+        torch._foreach_mul_(self.ema_params, self.smoothing)
+        torch._foreach_add_(self.ema_params, [p.detach() for p in params], alpha=1 - self.smoothing)
+
+
+def _not_applicable(name, why):
+    class _NA(Algorithm):
+        def __init__(self, *a, **k):
+            raise NotImplementedError(f"{name}: {why}")
+    _NA.__name__ = name
+    return _NA
+
+
+BlurPool = _not_applicable("BlurPool", "anti-aliased convolutions are a ResNet surgery; SwinV2 has none")
+ChannelsLast = _not_applicable("ChannelsLast", "SwinV2 activations are token-major already")
+ProgressiveResizing = _not_applicable("ProgressiveResizing",
+                                      "SwinV2 has a fixed input resolution (PatchEmbed asserts it)")
+PretrainedBackbone = _not_applicable("PretrainedBackbone", "W&B artifact download needs the network; "
+                                     "load swin:// checkpoints with swinv2.Checkpoint instead")

@@ -1,0 +1,82 @@
+// Shared device helpers for libhvk (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef __bf16 hvk_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float hvk_f32x4 __attribute__((ext_vector_type(4)));
+typedef short hvk_i16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short hvk_bf16;  // raw bf16 bits in memory
+
+#define HVK_LOG2E 1.4426950408889634f
+#define HVK_LDS_I16X4(p) ((__attribute__((address_space(3))) hvk_i16x4*)(p))
+
+// ---- host-side status plumbing (defined in capi.hip) ----------------------
+#ifdef __cplusplus
+extern "C" {
+#endif
+int hvk_set_error(int code, const char* fmt, ...);
+#ifdef __cplusplus
+}
+#endif
+
+#define HVK_OK 0
+#define HVK_EINVAL 1
+#define HVK_EUNSUPPORTED 2
+#define HVK_EHIP 3
+
+#define HVK_CHECK_LAUNCH(what)                                                   \
+  do {                                                                           \
+    hipError_t e_ = hipGetLastError();                                           \
+    if (e_ != hipSuccess)                                                        \
+      return hvk_set_error(HVK_EHIP, "%s: %s", what, hipGetErrorString(e_));     \
+  } while (0)
+
+// ---- bf16 <-> f32 ----------------------------------------------------------
+__device__ __forceinline__ float hvk_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hvk_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t hvk_f2bf(float f) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)f);  // RNE, v_cvt_pk_bf16_f32
+}
+__device__ __forceinline__ uint32_t hvk_pack2(float lo, float hi) {
+  return hvk_f2bf(lo) | (hvk_f2bf(hi) << 16);
+}
+__device__ __forceinline__ void hvk_unpack8(const uint4& v, float f[8]) {
+  f[0] = hvk_lo(v.x); f[1] = hvk_hi(v.x); f[2] = hvk_lo(v.y); f[3] = hvk_hi(v.y);
+  f[4] = hvk_lo(v.z); f[5] = hvk_hi(v.z); f[6] = hvk_lo(v.w); f[7] = hvk_hi(v.w);
+}
+__device__ __forceinline__ uint4 hvk_pack8(const float f[8]) {
+  return make_uint4(hvk_pack2(f[0], f[1]), hvk_pack2(f[2], f[3]), hvk_pack2(f[4], f[5]),
+                    hvk_pack2(f[6], f[7]));
+}
+
+// ---- MFMA 16x16x32 bf16 -> f32 --------------------------------------------
+// A lane l holds A[row l&15][k = 8(l>>4) + j], B lane l holds B[k = 8(l>>4) + j][col l&15],
+// D lane l holds D[row 4(l>>4) + r][col l&15], r = 0..3.
+__device__ __forceinline__ hvk_f32x4 hvk_mfma16(uint4 a, uint4 b, hvk_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(hvk_bf16x8, a),
+                                                 __builtin_bit_cast(hvk_bf16x8, b), c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, cols 4p..4p+3 of a
+// 4x16 bf16 block; lane i receives column i of the 4 rows (element q = row q).
+__device__ __forceinline__ uint2 hvk_tr_read(const hvk_bf16* lds) {
+  hvk_i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(HVK_LDS_I16X4(lds));
+  return __builtin_bit_cast(uint2, r);
+}
+
+__device__ __forceinline__ float hvk_wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// XCD-aware block id decode: logical (chunk, head) so that every head of a window chunk
+// lands in the same blockIdx%8 group (same XCD L2) and is dispatched back to back.
+// Grid = n_chunks_padded(multiple of 8) * n_heads.
+__device__ __forceinline__ void hvk_decode_chunk_head(int bid, int n_heads, int& chunk, int& head) {
+  const int xcd = bid & 7, loc = bid >> 3;
+  head = loc % n_heads;
+  chunk = (loc / n_heads) * 8 + xcd;
+}

@@ -1,0 +1,696 @@
+// Fused (shifted-)window cosine attention for SwinV2 on gfx950.
+//
+// Replaces, per block, the reference's eager sequence (swinv2.py):
+//   torch.roll(-s)                                  399-404
+//   window_partition + view                         69-83, 407-412
+//   F.normalize(q), F.normalize(k), q@k^T           229
+//   * exp(clamp(logit_scale, max=ln 100))           230-231
+//   + 16*sigmoid(cpb_mlp(table))[rpi]               233-247
+//   + shift mask (-100 across regions)              249-254, 357-388
+//   softmax, @v, transpose/reshape                  255-261
+//   window_reverse + torch.roll(+s)                 86-102, 420-429
+// The qkv and proj Linear layers are token-wise, so they commute with the
+// shift/partition permutation: the kernels read the UN-partitioned qkv token
+// tensor [B*H*W, 3C] and write the attention core output straight back to the
+// UN-partitioned token rows [B*H*W, C]; the roll/partition/reverse copies of the
+// reference never exist.  Windows are gathered by closed-form index math.
+//
+// Layout per (window, head) pair, one wave each: N = WIN^2 tokens padded to
+// NT = ceil(N/16) tiles of 16; head_dim = 32 = one K-step of
+// v_mfma_f32_16x16x32_bf16.  S^T = K Q^T keeps one query per lane column so
+// the softmax row reduction is in-lane (16 values) + 2 xor-shuffles; the S^T
+// accumulators feed P*V directly as the MFMA B operand (k-order permuted
+// consistently, see hvk_common.h); V^T comes from LDS through
+// ds_read_b64_tr_b16.  Bias (rpi gather of the CPB table) is expanded once per
+// workgroup into an LDS table laid out in accumulator order; the shift mask is
+// recomputed from region bits only on edge windows.
+#include "hvk_common.h"
+
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+
+struct WmsaGeom {
+  int B, H, W, C, nH, shift;
+  int nWh, nWw, n_windows;   // windows per image row/col, total windows (B*nWh*nWw)
+  int n_chunks, wpc;         // per head: chunks (un-padded) and windows per chunk
+};
+
+template <int WIN>
+struct WinCfg {
+  static constexpr int N = WIN * WIN;
+  static constexpr int NT = (N + 15) / 16;
+  static constexpr int NC = (NT + 1) / 2;  // 32-key chunks (one MFMA K-step each)
+  static constexpr int R = 2 * WIN - 1;
+  static constexpr int TAB = NT * NT * 256;  // floats in the accumulator-order bias table
+  static_assert(NT <= 4, "window larger than 8 needs the streamed-key variant");
+};
+
+// Expand 16*sigmoid(cpb) [(2w-1)^2] for one head into accumulator order:
+// tab[((qi*NT + ki)*64 + lane)*4 + r] = log2e * bias(q = 16qi + (lane&15), key = 16ki + 4(lane>>4) + r)
+// padded keys -> -inf (P = 0), padded queries -> 0 (never stored).
+template <int WIN>
+__device__ void build_bias_table(float* tab, const float* __restrict__ src) {
+  using K = WinCfg<WIN>;
+  for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
+    const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
+    const int qi = blk / K::NT, ki = blk % K::NT;
+    const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
+    float v;
+    if (key >= K::N) {
+      v = -INFINITY;
+    } else if (q >= K::N) {
+      v = 0.f;
+    } else {
+      const int idx = (q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1);
+      v = src[idx] * HVK_LOG2E;
+    }
+    tab[e] = v;
+  }
+}
+
+// token row (in the un-shifted [B*H*W] token order) of window position t
+__device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh, int ww, int win,
+                                                int t) {
+  int y = wh * win + t / win + g.shift;
+  int x = ww * win + t % win + g.shift;
+  if (y >= g.H) y -= g.H;
+  if (x >= g.W) x -= g.W;
+  return (b * g.H + y) * g.W + x;
+}
+
+// L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
+__device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm) {
+  float f[8];
+  hvk_unpack8(v, f);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  ss += __shfl_xor(ss, 16);
+  ss += __shfl_xor(ss, 32);
+  rnorm = 1.f / fmaxf(sqrtf(ss), 1e-12f);  // F.normalize: x / max(||x||, eps)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= rnorm;
+  return hvk_pack8(f);
+}
+
+// Region bit of a window-local coordinate in the last window row/col (swinv2.py:359-375).
+template <int WIN>
+__device__ __forceinline__ uint32_t key_band_bits(int g, int shift, bool rows) {
+  using K = WinCfg<WIN>;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = 16 * ki + 4 * g + r;
+      const int c = rows ? key / WIN : key % WIN;
+      if (key < K::N && c >= WIN - shift) bits |= 1u << (ki * 4 + r);
+    }
+  return bits;
+}
+
+// bit (ki*4 + r) set <=> key 16ki + 4g + r lies in a different shift region than query q
+__device__ __forceinline__ uint32_t mask_bits(uint32_t krow, uint32_t kcol, int q, int lim, int win,
+                                              bool edge_r, bool edge_c) {
+  const uint32_t qr = (q / win) >= lim ? ~0u : 0u, qc = (q % win) >= lim ? ~0u : 0u;
+  return (edge_r ? (krow ^ qr) : 0u) | (edge_c ? (kcol ^ qc) : 0u);
+}
+
+struct FwdArgs {
+  const hvk_bf16* qkv;       // [T, 3C]
+  hvk_bf16* out;             // [T, C]
+  const float* bias;         // [nH, R*R]   16*sigmoid(cpb)
+  const float* scale;        // [nH]        exp(clamp(logit_scale))
+  WmsaGeom g;
+};
+
+template <int WIN>
+__global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
+  using K = WinCfg<WIN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WmsaGeom& g = a.g;
+  int chunk, h;
+  hvk_decode_chunk_head(blockIdx.x, g.nH, chunk, h);
+  if (chunk >= g.n_chunks) return;
+  const int w0 = chunk * g.wpc, w1 = min(w0 + g.wpc, g.n_windows);
+  if (w0 >= w1) return;
+
+  float* btab = reinterpret_cast<float*>(smem);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  hvk_bf16* vst = reinterpret_cast<hvk_bf16*>(smem + K::TAB * 4) + wave * (32 * K::NC * 32);
+  build_bias_table<WIN>(btab, a.bias + (size_t)h * K::R * K::R);
+  __syncthreads();
+
+  const int li = lane & 15, gq = lane >> 4;
+  const int C = g.C, C3 = 3 * g.C;
+  const float sc2 = a.scale[h] * HVK_LOG2E;
+  const float mask2 = -100.f * HVK_LOG2E;
+  const uint32_t krow = g.shift ? key_band_bits<WIN>(gq, g.shift, true) : 0u;
+  const uint32_t kcol = g.shift ? key_band_bits<WIN>(gq, g.shift, false) : 0u;
+  const int per_img = g.nWh * g.nWw;
+
+  for (int w = w0 + wave; w < w1; w += kWaves) {
+    const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    int row[K::NT];
+    uint4 qf[K::NT], kf[K::NT], vf[K::NT];
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      const int t = 16 * i + li;
+      row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
+      if (t < K::N) {
+        const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
+        qf[i] = *reinterpret_cast<const uint4*>(p);
+        kf[i] = *reinterpret_cast<const uint4*>(p + C);
+        vf[i] = *reinterpret_cast<const uint4*>(p + 2 * C);
+      } else {
+        qf[i] = kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    float rn;
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      qf[i] = l2_normalize(qf[i], rn);
+      kf[i] = l2_normalize(kf[i], rn);
+      *reinterpret_cast<uint4*>(vst + (16 * i + li) * 32 + 8 * gq) = vf[i];
+    }
+#pragma unroll
+    for (int i = K::NT; i < 2 * K::NC; ++i)
+      *reinterpret_cast<uint4*>(vst + (16 * i + li) * 32 + 8 * gq) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // V^T fragments (A operand of O^T = V^T P^T), key order per chunk c, lane group g, slot j:
+    // key(g, j) = 32c + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+    uint4 vt[K::NC][2];
+#pragma unroll
+    for (int c = 0; c < K::NC; ++c)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const hvk_bf16* base = vst + (32 * c + 4 * gq + (li >> 2)) * 32 + 16 * dt + 4 * (li & 3);
+        const uint2 lo = hvk_tr_read(base), hi = hvk_tr_read(base + 16 * 32);
+        vt[c][dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+
+#pragma unroll
+    for (int qi = 0; qi < K::NT; ++qi) {
+      // keep one query tile live at a time and the bias-table reads inside the loop (VGPR budget)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      hvk_f32x4 s[K::NT];
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) s[ki] = hvk_mfma16(kf[ki], qf[qi], hvk_f32x4{0, 0, 0, 0});
+      const int q = 16 * qi + li;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) {
+        const float4 bb = *reinterpret_cast<const float4*>(btab + ((qi * K::NT + ki) * 64 + lane) * 4);
+        s[ki][0] = s[ki][0] * sc2 + bb.x;
+        s[ki][1] = s[ki][1] * sc2 + bb.y;
+        s[ki][2] = s[ki][2] * sc2 + bb.z;
+        s[ki][3] = s[ki][3] * sc2 + bb.w;
+      }
+      if (edge_r || edge_c) {  // wave-uniform: only the last window row / column carries a mask
+        const uint32_t mm = mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c);
+#pragma unroll
+        for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[ki][r] += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[ki][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[ki][r] - mx);
+          s[ki][r] = p;
+          sum += p;
+        }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      hvk_f32x4 o[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c) {
+        const hvk_f32x4 a0 = s[2 * c];
+        const hvk_f32x4 a1 = (2 * c + 1 < K::NT) ? s[2 * c + 1] : hvk_f32x4{0, 0, 0, 0};
+        const uint4 pf = make_uint4(hvk_pack2(a0[0], a0[1]), hvk_pack2(a0[2], a0[3]),
+                                    hvk_pack2(a1[0], a1[1]), hvk_pack2(a1[2], a1[3]));
+        o[0] = hvk_mfma16(vt[c][0], pf, o[0]);
+        o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
+      }
+      if (q < K::N) {
+        const float inv = 1.f / sum;
+        hvk_bf16* dst = a.out + (size_t)row[qi] * C + h * 32 + 4 * gq;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          *reinterpret_cast<uint2*>(dst + 16 * dt) =
+              make_uint2(hvk_pack2(o[dt][0] * inv, o[dt][1] * inv),
+                         hvk_pack2(o[dt][2] * inv, o[dt][3] * inv));
+      }
+    }
+  }
+}
+
+struct BwdArgs {
+  const hvk_bf16* qkv;       // [T, 3C]
+  const hvk_bf16* dout;      // [T, C]   gradient of the attention core output
+  hvk_bf16* dqkv;            // [T, 3C]
+  const float* bias;         // [nH, R*R]
+  const float* scale;        // [nH]
+  float* dbias_acc;          // [nH, TAB] accumulator-order partial sums (zeroed by launcher)
+  float* dscale;             // [nH] (zeroed by launcher)
+  WmsaGeom g;
+};
+
+// Backward, one wave per (window, head), recomputing P from q, k (no saved
+// probabilities).  Phase A (query on the lane): S^T, P^T, dP^T = V dO^T,
+// dS^T = P (dP - rowsum(P dP)), dQ^ = scale dS K^ (K^T via tr-reads).
+// Phase B (key on the lane): dV^T = dO^T P, dK^T = Q^T (scale dS), both with
+// the P / dS images staged in LDS and read transposed.
+template <int WIN>
+__global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
+  using K = WinCfg<WIN>;
+  constexpr int ROWS = 32 * K::NC;                 // padded token rows in LDS images
+  constexpr int WAVE_LDS = ROWS * 32 * 3 + ROWS * ROWS * 2;  // q^, k^, dO [ROWS][32]; P, dS [ROWS][ROWS]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WmsaGeom& g = a.g;
+  int chunk, h;
+  hvk_decode_chunk_head(blockIdx.x, g.nH, chunk, h);
+  if (chunk >= g.n_chunks) return;
+  const int w0 = chunk * g.wpc, w1 = min(w0 + g.wpc, g.n_windows);
+  if (w0 >= w1) return;
+
+  float* btab = reinterpret_cast<float*>(smem);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  hvk_bf16* qs = reinterpret_cast<hvk_bf16*>(smem + K::TAB * 4) + wave * WAVE_LDS;
+  hvk_bf16* ks = qs + ROWS * 32;
+  hvk_bf16* dos = ks + ROWS * 32;
+  hvk_bf16* ps = dos + ROWS * 32;
+  hvk_bf16* dss = ps + ROWS * ROWS;
+  build_bias_table<WIN>(btab, a.bias + (size_t)h * K::R * K::R);
+  // zero the padded rows of the staged images once (never rewritten)
+  for (int e = lane; e < ROWS * 32 * 3 + ROWS * ROWS * 2; e += 64) qs[e] = 0;
+  __syncthreads();
+
+  const int li = lane & 15, gq = lane >> 4;
+  const int C = g.C, C3 = 3 * g.C;
+  const float scale = a.scale[h];
+  const float sc2 = scale * HVK_LOG2E;
+  const float mask2 = -100.f * HVK_LOG2E;
+  const uint32_t krow = g.shift ? key_band_bits<WIN>(gq, g.shift, true) : 0u;
+  const uint32_t kcol = g.shift ? key_band_bits<WIN>(gq, g.shift, false) : 0u;
+  const int per_img = g.nWh * g.nWw;
+
+  hvk_f32x4 dbias[K::NT][K::NT];
+#pragma unroll
+  for (int qi = 0; qi < K::NT; ++qi)
+#pragma unroll
+    for (int ki = 0; ki < K::NT; ++ki) dbias[qi][ki] = hvk_f32x4{0, 0, 0, 0};
+  float dscale = 0.f;
+
+  for (int w = w0 + wave; w < w1; w += kWaves) {
+    const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    int row[K::NT];
+    uint4 qf[K::NT], kf[K::NT], vf[K::NT], df[K::NT];
+    float rnq[K::NT], rnk[K::NT];
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      const int t = 16 * i + li;
+      row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
+      if (t < K::N) {
+        const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
+        qf[i] = *reinterpret_cast<const uint4*>(p);
+        kf[i] = *reinterpret_cast<const uint4*>(p + C);
+        vf[i] = *reinterpret_cast<const uint4*>(p + 2 * C);
+        df[i] = *reinterpret_cast<const uint4*>(a.dout + (size_t)row[i] * C + h * 32 + 8 * gq);
+      } else {
+        qf[i] = kf[i] = vf[i] = df[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      qf[i] = l2_normalize(qf[i], rnq[i]);
+      kf[i] = l2_normalize(kf[i], rnk[i]);
+      *reinterpret_cast<uint4*>(qs + (16 * i + li) * 32 + 8 * gq) = qf[i];
+      *reinterpret_cast<uint4*>(ks + (16 * i + li) * 32 + 8 * gq) = kf[i];
+      *reinterpret_cast<uint4*>(dos + (16 * i + li) * 32 + 8 * gq) = df[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // K^T fragments for dQ^T = K^T dS^T (k = key, permuted order as in the forward)
+    uint4 kt_frag[K::NC][2];
+#pragma unroll
+    for (int c = 0; c < K::NC; ++c)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const hvk_bf16* base = ks + (32 * c + 4 * gq + (li >> 2)) * 32 + 16 * dt + 4 * (li & 3);
+        const uint2 lo = hvk_tr_read(base), hi = hvk_tr_read(base + 16 * 32);
+        kt_frag[c][dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+
+    // ---------------- phase A: one query tile at a time, query on the lane
+#pragma unroll
+    for (int qi = 0; qi < K::NT; ++qi) {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      hvk_f32x4 s[K::NT], dp[K::NT];
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) {
+        s[ki] = hvk_mfma16(kf[ki], qf[qi], hvk_f32x4{0, 0, 0, 0});   // cos(q, k)
+        dp[ki] = hvk_mfma16(vf[ki], df[qi], hvk_f32x4{0, 0, 0, 0});  // dO . V
+      }
+      const int q = 16 * qi + li;
+      float p[K::NT][4];
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) {
+        const float4 bb = *reinterpret_cast<const float4*>(btab + ((qi * K::NT + ki) * 64 + lane) * 4);
+        p[ki][0] = s[ki][0] * sc2 + bb.x;
+        p[ki][1] = s[ki][1] * sc2 + bb.y;
+        p[ki][2] = s[ki][2] * sc2 + bb.z;
+        p[ki][3] = s[ki][3] * sc2 + bb.w;
+      }
+      if (edge_r || edge_c) {
+        const uint32_t mm = mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c);
+#pragma unroll
+        for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[ki][r] += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, p[ki][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[ki][r] = exp2f(p[ki][r] - mx);
+          sum += p[ki][r];
+        }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      const float inv = 1.f / sum;
+      float delta = 0.f;
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[ki][r] *= inv;
+          delta += p[ki][r] * dp[ki][r];
+        }
+      delta += __shfl_xor(delta, 16);
+      delta += __shfl_xor(delta, 32);
+      float ds[K::NT][4];
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          ds[ki][r] = p[ki][r] * (dp[ki][r] - delta);
+          dbias[qi][ki][r] += ds[ki][r];
+          dscale += ds[ki][r] * s[ki][r];
+        }
+        // stage P and scale*dS as [query][key] rows for phase B
+        const int off = q * ROWS + 16 * ki + 4 * gq;
+        *reinterpret_cast<uint2*>(ps + off) =
+            make_uint2(hvk_pack2(p[ki][0], p[ki][1]), hvk_pack2(p[ki][2], p[ki][3]));
+        *reinterpret_cast<uint2*>(dss + off) =
+            make_uint2(hvk_pack2(scale * ds[ki][0], scale * ds[ki][1]),
+                       hvk_pack2(scale * ds[ki][2], scale * ds[ki][3]));
+      }
+      // dQ^T = K^T (scale dS^T)
+      hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c) {
+        const bool has1 = 2 * c + 1 < K::NT;
+        const uint4 bf = make_uint4(
+            hvk_pack2(scale * ds[2 * c][0], scale * ds[2 * c][1]),
+            hvk_pack2(scale * ds[2 * c][2], scale * ds[2 * c][3]),
+            has1 ? hvk_pack2(scale * ds[2 * c + 1][0], scale * ds[2 * c + 1][1]) : 0u,
+            has1 ? hvk_pack2(scale * ds[2 * c + 1][2], scale * ds[2 * c + 1][3]) : 0u);
+        dq[0] = hvk_mfma16(kt_frag[c][0], bf, dq[0]);
+        dq[1] = hvk_mfma16(kt_frag[c][1], bf, dq[1]);
+      }
+      // normalize backward: dq = (dq^ - q^ (q^ . dq^)) / max(||q||, eps)
+      float qh[2][4], dot = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const uint2 v = *reinterpret_cast<const uint2*>(qs + q * 32 + 16 * dt + 4 * gq);
+        qh[dt][0] = hvk_lo(v.x); qh[dt][1] = hvk_hi(v.x);
+        qh[dt][2] = hvk_lo(v.y); qh[dt][3] = hvk_hi(v.y);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dot += qh[dt][r] * dq[dt][r];
+      }
+      dot += __shfl_xor(dot, 16);
+      dot += __shfl_xor(dot, 32);
+      if (rnq[qi] >= 1e12f) dot = 0.f;  // ||q|| <= eps: x / eps, no projection term
+      if (q < K::N) {
+        hvk_bf16* dst = a.dqkv + (size_t)row[qi] * C3 + h * 32 + 4 * gq;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[qi];
+          *reinterpret_cast<uint2*>(dst + 16 * dt) =
+              make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    // ---------------- phase B: one key tile at a time, key on the lane
+    // query chunk c, slot (g, j): q(g, j) = 32c + (j < 4 ? 4g + j : 16 + 4g + j - 4)
+#pragma unroll
+    for (int kt = 0; kt < K::NT; ++kt) {
+      hvk_f32x4 dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c) {
+        const int rq = 32 * c + 4 * gq + (li >> 2);
+        const hvk_bf16* pb = ps + rq * ROWS + 16 * kt + 4 * (li & 3);
+        const hvk_bf16* db = dss + rq * ROWS + 16 * kt + 4 * (li & 3);
+        uint2 lo = hvk_tr_read(pb), hi = hvk_tr_read(pb + 16 * ROWS);
+        const uint4 pfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        lo = hvk_tr_read(db); hi = hvk_tr_read(db + 16 * ROWS);
+        const uint4 dsfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const hvk_bf16* ob = dos + rq * 32 + 16 * dt + 4 * (li & 3);
+          lo = hvk_tr_read(ob); hi = hvk_tr_read(ob + 16 * 32);
+          dv[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), pfr, dv[dt]);
+          const hvk_bf16* qb = qs + rq * 32 + 16 * dt + 4 * (li & 3);
+          lo = hvk_tr_read(qb); hi = hvk_tr_read(qb + 16 * 32);
+          dk[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), dsfr, dk[dt]);
+        }
+      }
+      const int key = 16 * kt + li;
+      float kh[2][4], dot = 0.f;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const uint2 v = *reinterpret_cast<const uint2*>(ks + key * 32 + 16 * dt + 4 * gq);
+        kh[dt][0] = hvk_lo(v.x); kh[dt][1] = hvk_hi(v.x);
+        kh[dt][2] = hvk_lo(v.y); kh[dt][3] = hvk_hi(v.y);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dot += kh[dt][r] * dk[dt][r];
+      }
+      dot += __shfl_xor(dot, 16);
+      dot += __shfl_xor(dot, 32);
+      if (rnk[kt] >= 1e12f) dot = 0.f;
+      if (key < K::N) {
+        hvk_bf16* dst = a.dqkv + (size_t)row[kt] * C3 + h * 32 + 4 * gq;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rnk[kt];
+          *reinterpret_cast<uint2*>(dst + C + 16 * dt) =
+              make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+          *reinterpret_cast<uint2*>(dst + 2 * C + 16 * dt) =
+              make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- workgroup reduction of the bias / scale gradients, then one atomic per entry
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem + K::TAB * 4) + wave * K::TAB;  // reuses staging
+  static_assert(K::TAB * 4 <= WAVE_LDS * 2, "reduction buffer must fit in the wave's staging");
+#pragma unroll
+  for (int qi = 0; qi < K::NT; ++qi)
+#pragma unroll
+    for (int ki = 0; ki < K::NT; ++ki)
+      *reinterpret_cast<float4*>(red + ((qi * K::NT + ki) * 64 + lane) * 4) =
+          make_float4(dbias[qi][ki][0], dbias[qi][ki][1], dbias[qi][ki][2], dbias[qi][ki][3]);
+  __syncthreads();
+  const float* red0 = reinterpret_cast<const float*>(smem + K::TAB * 4);
+  float* dst = a.dbias_acc + (size_t)h * K::TAB;
+  for (int e = threadIdx.x; e < K::TAB; e += kThreads) {
+    float v = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < kWaves; ++wv) v += red0[wv * K::TAB + e];
+    atomicAdd(dst + e, v);
+  }
+  dscale = hvk_wave_sum(dscale);
+  if (lane == 0) atomicAdd(a.dscale + h, dscale);
+}
+
+// Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R].
+template <int WIN>
+__global__ __launch_bounds__(256) void wmsa_dbias_finalize_kernel(const float* __restrict__ acc,
+                                                                  float* __restrict__ dtab) {
+  using K = WinCfg<WIN>;
+  __shared__ float bins[K::R * K::R];
+  const int h = blockIdx.x;
+  for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) bins[i] = 0.f;
+  __syncthreads();
+  for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
+    const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
+    const int qi = blk / K::NT, ki = blk % K::NT;
+    const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
+    if (q < K::N && key < K::N) {
+      const int idx = (q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1);
+      atomicAdd(&bins[idx], acc[(size_t)h * K::TAB + e]);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) dtab[(size_t)h * K::R * K::R + i] = bins[i];
+}
+
+template <int WIN>
+constexpr size_t fwd_lds_bytes() {
+  return WinCfg<WIN>::TAB * 4 + kWaves * (32 * WinCfg<WIN>::NC * 32) * 2;
+}
+template <int WIN>
+constexpr size_t bwd_lds_bytes() {
+  constexpr int ROWS = 32 * WinCfg<WIN>::NC;
+  return WinCfg<WIN>::TAB * 4 + kWaves * (size_t)(ROWS * 32 * 3 + ROWS * ROWS * 2) * 2;
+}
+
+int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int target_wgs, WmsaGeom& g) {
+  if (B <= 0 || H <= 0 || W <= 0 || nH <= 0)
+    return hvk_set_error(HVK_EINVAL, "wmsa: bad shape B=%d H=%d W=%d nH=%d", B, H, W, nH);
+  if (C != 32 * nH)
+    return hvk_set_error(HVK_EUNSUPPORTED, "wmsa: head_dim must be 32 (C=%d, nH=%d)", C, nH);
+  if (H % win || W % win)
+    return hvk_set_error(HVK_EINVAL, "wmsa: H=%d W=%d not divisible by window %d", H, W, win);
+  if (shift < 0 || shift >= win)
+    return hvk_set_error(HVK_EINVAL, "wmsa: shift %d outside [0, %d)", shift, win);
+  g.B = B; g.H = H; g.W = W; g.C = C; g.nH = nH; g.shift = shift;
+  g.nWh = H / win; g.nWw = W / win;
+  g.n_windows = B * g.nWh * g.nWw;
+  int chunks = (target_wgs + nH - 1) / nH;
+  chunks = chunks < 1 ? 1 : chunks;
+  g.wpc = (g.n_windows + chunks - 1) / chunks;
+  g.n_chunks = (g.n_windows + g.wpc - 1) / g.wpc;
+  return HVK_OK;
+}
+
+template <int WIN>
+int launch_fwd(const FwdArgs& a, hipStream_t st) {
+  const int padded = (a.g.n_chunks + 7) / 8 * 8;
+  const size_t lds = fwd_lds_bytes<WIN>();
+  hipLaunchKernelGGL(wmsa_fwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
+  HVK_CHECK_LAUNCH("wmsa_fwd");
+  return HVK_OK;
+}
+
+template <int WIN>
+int launch_bwd(const BwdArgs& a, float* dbias_table, hipStream_t st) {
+  const int padded = (a.g.n_chunks + 7) / 8 * 8;
+  const size_t lds = bwd_lds_bytes<WIN>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_kernel<WIN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(wmsa_bwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
+  HVK_CHECK_LAUNCH("wmsa_bwd");
+  hipLaunchKernelGGL(wmsa_dbias_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st,
+                     a.dbias_acc, dbias_table);
+  HVK_CHECK_LAUNCH("wmsa_dbias_finalize");
+  return HVK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
+  const int n = window * window, nt = (n + 15) / 16;
+  return (size_t)num_heads * nt * nt * 256 * sizeof(float);
+}
+
+int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale, int B,
+                 int H, int W, int C, int num_heads, int window, int shift, void* stream) {
+  if (!qkv || !out || !bias_table || !scale)
+    return hvk_set_error(HVK_EINVAL, "hvk_wmsa_fwd: null pointer");
+  FwdArgs a;
+  a.qkv = static_cast<const hvk_bf16*>(qkv);
+  a.out = static_cast<hvk_bf16*>(out);
+  a.bias = bias_table;
+  a.scale = scale;
+  // ~16 windows per workgroup (4 per wave)
+  const int nwin = B * (H / (window > 0 ? window : 1)) * (W / (window > 0 ? window : 1));
+  const int target = ((nwin + 15) / 16) * num_heads;
+  int rc = make_geom(B, H, W, C, num_heads, window, shift, target, a.g);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (window) {
+    case 7: return launch_fwd<7>(a, st);
+    case 8: return launch_fwd<8>(a, st);
+    case 6: return launch_fwd<6>(a, st);
+    case 4: return launch_fwd<4>(a, st);
+    default:
+      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8)", window);
+  }
+}
+
+int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bias_table,
+                 const float* scale, float* dbias_table, float* dscale, float* workspace,
+                 size_t workspace_bytes, int B, int H, int W, int C, int num_heads, int window,
+                 int shift, void* stream) {
+  if (!qkv || !dout || !dqkv || !bias_table || !scale || !dbias_table || !dscale || !workspace)
+    return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: null pointer");
+  if (workspace_bytes < hvk_wmsa_bwd_workspace_bytes(num_heads, window))
+    return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: workspace too small");
+  BwdArgs a;
+  a.qkv = static_cast<const hvk_bf16*>(qkv);
+  a.dout = static_cast<const hvk_bf16*>(dout);
+  a.dqkv = static_cast<hvk_bf16*>(dqkv);
+  a.bias = bias_table;
+  a.scale = scale;
+  a.dbias_acc = workspace;
+  a.dscale = dscale;
+  // one resident 4-wave workgroup per CU (LDS-bound), two rounds over the chip
+  int rc = make_geom(B, H, W, C, num_heads, window, shift, 512, a.g);
+  if (rc) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hipMemsetAsync(workspace, 0, hvk_wmsa_bwd_workspace_bytes(num_heads, window), st) != hipSuccess ||
+      hipMemsetAsync(dscale, 0, sizeof(float) * num_heads, st) != hipSuccess)
+    return hvk_set_error(HVK_EHIP, "hvk_wmsa_bwd: memset failed");
+  switch (window) {
+    case 7: return launch_bwd<7>(a, dbias_table, st);
+    case 8: return launch_bwd<8>(a, dbias_table, st);
+    case 6: return launch_bwd<6>(a, dbias_table, st);
+    case 4: return launch_bwd<4>(a, dbias_table, st);
+    default:
+      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: window %d not built (4,6,7,8)", window);
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,234 @@
+"""autograd Functions over libhvk's C ABI (include/hvk.h).
+
+Every Function here launches only HIP kernels from libhvk.so on PyTorch's
+current stream; tensors are plumbing (PyTorch owns the memory).  There is no
+eager/CPU fallback: a CPU tensor or a missing library raises.
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream
+
+
+_TIMER = None  # list of (kind, start_event, end_event) while a bench timing window is open
+
+
+def set_kernel_timer(timer):
+    """Open (list) / close (None) a timing window: every W-MSA launch is bracketed by HIP
+    events on the stream it is launched on (bench.py roofline)."""
+    global _TIMER
+    _TIMER = timer
+
+
+def _timed(kind, fn):
+    if _TIMER is None:
+        return fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    r = fn()
+    e.record()
+    _TIMER.append((kind, s, e))
+    return r
+
+
+def _bf16(t):
+    t = t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+    return t.contiguous()
+
+
+def _f32(t):
+    t = t if t.dtype == torch.float32 else t.float()
+    return t.contiguous()
+
+
+# --------------------------------------------------------------------------- W-MSA
+class WindowAttentionCore(torch.autograd.Function):
+    """Shifted-window cosine attention core on un-partitioned tokens.
+
+    qkv [B, H*W, 3C] bf16 -> out [B, H*W, C] bf16.  Stands in for
+    swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h)."""
+
+    @staticmethod
+    def forward(ctx, qkv, bias_table, scale, H, W, num_heads, window, shift):
+        B, L, C3 = qkv.shape
+        C = C3 // 3
+        if L != H * W:
+            raise ValueError(f"token count {L} != {H}*{W}")
+        qkv = _bf16(qkv)
+        bias_table = _f32(bias_table)
+        scale = _f32(scale)
+        out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
+        _timed("wmsa_fwd", lambda: call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(bias_table),
+                                        ptr(scale), B, H, W, C, num_heads, window, shift,
+                                        stream()))
+        ctx.save_for_backward(qkv, bias_table, scale)
+        ctx.geom = (B, H, W, C, num_heads, window, shift)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, bias_table, scale = ctx.saved_tensors
+        B, H, W, C, nh, win, shift = ctx.geom
+        dout = _bf16(dout)
+        dqkv = torch.empty_like(qkv)
+        dtab = torch.empty_like(bias_table)
+        dscale = torch.empty_like(scale)
+        ws_bytes = _lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
+        ws = torch.empty(ws_bytes // 4, device=qkv.device, dtype=torch.float32)
+        _timed("wmsa_bwd", lambda: call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(dqkv),
+                                        ptr(bias_table), ptr(scale), ptr(dtab), ptr(dscale),
+                                        ptr(ws), ws_bytes, B, H, W, C, nh, win, shift,
+                                        stream()))
+        return dqkv, dtab, dscale, None, None, None, None, None
+
+
+def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift):
+    return WindowAttentionCore.apply(qkv, bias_table, scale, H, W, num_heads, window, shift)
+
+
+# --------------------------------------------------------------------------- LayerNorm
+class LayerNormResidual(torch.autograd.Function):
+    """x = x0 + s[b] * LayerNorm(a); returns (x f32, x bf16 copy)."""
+
+    @staticmethod
+    def forward(ctx, a, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        C = a.shape[-1]
+        rows = a.numel() // C
+        a = _bf16(a)
+        gamma, beta = _f32(gamma), _f32(beta)
+        if x0 is not None:
+            x0 = _f32(x0)
+        if sample_scale is not None:
+            sample_scale = _f32(sample_scale)
+        x = torch.empty(a.shape, device=a.device, dtype=torch.float32)
+        xb = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16)
+        mean = torch.empty(rows, device=a.device, dtype=torch.float32)
+        rstd = torch.empty(rows, device=a.device, dtype=torch.float32)
+        call("hvk_ln_residual_fwd", ptr(a), ptr(x0), ptr(gamma), ptr(beta), ptr(sample_scale),
+             rows, C, rows_per_sample, float(eps), ptr(x), ptr(xb), ptr(mean), ptr(rstd),
+             stream())
+        ctx.save_for_backward(a, gamma, sample_scale, mean, rstd)
+        ctx.has_x0 = x0 is not None
+        ctx.rps = rows_per_sample
+        return x, xb
+
+    @staticmethod
+    def backward(ctx, gx, gxb):
+        a, gamma, sample_scale, mean, rstd = ctx.saved_tensors
+        C = a.shape[-1]
+        rows = a.numel() // C
+        gx = _f32(gx) if gx is not None else None
+        gxb = _bf16(gxb) if gxb is not None else None
+        if gx is None and gxb is None:
+            return (None,) * 7
+        ga = torch.empty_like(a)
+        gx0 = torch.empty(a.shape, device=a.device, dtype=torch.float32) if ctx.has_x0 else None
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(gamma)
+        ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
+        ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
+        call("hvk_ln_residual_bwd", ptr(a), ptr(gamma), ptr(sample_scale), ptr(mean), ptr(rstd),
+             ptr(gx), ptr(gxb), rows, C, ctx.rps, ptr(gx0), ptr(ga), ptr(dgamma), ptr(dbeta),
+             ptr(ws), ws_bytes, stream())
+        return ga, gx0, dgamma, dbeta, None, None, None
+
+
+def layer_norm_residual(a, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5):
+    return LayerNormResidual.apply(a, x0, gamma, beta, sample_scale, rows_per_sample, eps)
+
+
+# --------------------------------------------------------------------------- PatchMerging
+class PatchMergeGather(torch.autograd.Function):
+    """[B, H*W, C] -> [B, H/2*W/2, 4C] in the concat order of swinv2.py:486-490."""
+
+    @staticmethod
+    def forward(ctx, x, H, W):
+        B, L, C = x.shape
+        x = _bf16(x)
+        out = torch.empty((B, L // 4, 4 * C), device=x.device, dtype=torch.bfloat16)
+        call("hvk_patch_merge_gather", ptr(x), ptr(out), B, H, W, C, stream())
+        ctx.geom = (B, H, W, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, H, W, C = ctx.geom
+        g = _bf16(g)
+        gx = torch.empty((B, H * W, C), device=g.device, dtype=torch.bfloat16)
+        call("hvk_patch_merge_scatter", ptr(g), ptr(gx), B, H, W, C, stream())
+        return gx, None, None
+
+
+def patch_merge_gather(x, H, W):
+    return PatchMergeGather.apply(x, H, W)
+
+
+# --------------------------------------------------------------------------- losses
+class MultitaskCE(torch.autograd.Function):
+    """sum_h coeff[h] * mean_b CE(logits[:, off[h]:off[h+1]], target_h)."""
+
+    @staticmethod
+    def forward(ctx, logits, head_off, coeff, targets, soft):
+        logits = _f32(logits)
+        B, ld = logits.shape
+        nh = head_off.numel() - 1
+        row_loss = torch.empty((nh, B), device=logits.device, dtype=torch.float32)
+        lse = torch.empty((nh, B), device=logits.device, dtype=torch.float32)
+        call("hvk_multitask_ce_fwd", ptr(logits), ld, B, nh, ptr(head_off), ptr(targets),
+             ptr(soft), ptr(row_loss), ptr(lse), stream())
+        ctx.save_for_backward(logits, head_off, coeff, targets, soft, lse)
+        return (row_loss.mean(dim=1) * coeff).sum()
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, head_off, coeff, targets, soft, lse = ctx.saved_tensors
+        B, ld = logits.shape
+        nh = head_off.numel() - 1
+        dlogits = torch.empty_like(logits)
+        gout = _f32(gout.reshape(1))
+        call("hvk_multitask_ce_bwd", ptr(logits), ld, B, nh, ptr(head_off), ptr(targets),
+             ptr(soft), ptr(lse), ptr(coeff), ptr(gout), ptr(dlogits), stream())
+        return dlogits, None, None, None, None
+
+
+def multitask_cross_entropy(logits, head_off, coeff, targets=None, soft=None):
+    if (targets is None) == (soft is None):
+        raise ValueError("exactly one of hard targets / soft targets")
+    if targets is not None:
+        targets = targets.to(torch.int64).contiguous()
+    if soft is not None:
+        soft = _f32(soft)
+    return MultitaskCE.apply(logits, head_off, coeff, targets, soft)
+
+
+class HierarchicalCE(torch.autograd.Function):
+    """HXE over leaf logits [B, L]; see include/hvk.h for the definition."""
+
+    @staticmethod
+    def forward(ctx, logits, targets, perm, node_start, node_end, tier_base, level_coeff):
+        logits = _f32(logits)
+        B, L = logits.shape
+        row_loss = torch.empty(B, device=logits.device, dtype=torch.float32)
+        lse = torch.empty((B, 8), device=logits.device, dtype=torch.float32)
+        call("hvk_hxe_fwd", ptr(logits), B, L, ptr(perm), ptr(targets), ptr(node_start),
+             ptr(node_end), ptr(tier_base), ptr(level_coeff), ptr(row_loss), ptr(lse), stream())
+        ctx.save_for_backward(logits, targets, perm, node_start, node_end, tier_base,
+                              level_coeff, lse)
+        ctx.has_perm = perm is not None
+        return row_loss.mean()
+
+    @staticmethod
+    def backward(ctx, gout):
+        logits, targets, perm, node_start, node_end, tier_base, level_coeff, lse = ctx.saved_tensors
+        B, L = logits.shape
+        dlogits = torch.empty_like(logits)
+        gout = _f32(gout.reshape(1))
+        call("hvk_hxe_bwd", ptr(logits), B, L, ptr(perm if ctx.has_perm else None), ptr(targets),
+             ptr(node_start), ptr(node_end), ptr(tier_base), ptr(level_coeff), ptr(lse),
+             ptr(gout), ptr(dlogits), stream())
+        return dlogits, None, None, None, None, None, None
+
+
+def hierarchical_cross_entropy(logits, targets, perm, node_start, node_end, tier_base, level_coeff):
+    return HierarchicalCE.apply(logits, targets.to(torch.int64).contiguous(), perm, node_start,
+                                node_end, tier_base, level_coeff)

@@ -1,0 +1,117 @@
+/* libhvk -- MI355X (gfx950) kernels for the SwinV2 + taxonomy-loss training hot path of
+ * samuelstevens/hierarchical-vision, behind a plain C ABI.
+ *
+ * Conventions (every entry point):
+ *  - returns 0 on success, else HVK_EINVAL(1) / HVK_EUNSUPPORTED(2) / HVK_EHIP(3);
+ *    hvk_last_error_string() gives the text (thread-local).
+ *  - all pointers are device pointers owned by the caller (the PyTorch caching allocator);
+ *    the library never allocates device memory.  Tensors are contiguous row-major.
+ *  - `stream` is a hipStream_t; work is enqueued asynchronously, nothing synchronises.
+ *  - "bf16" buffers hold raw bfloat16 bits; "f32" buffers hold float.
+ *
+ * The reference has no native code: each entry point replaces an eager
+ * PyTorch op sequence; the citation names the reference lines it stands in for.
+ */
+#ifndef HVK_H_
+#define HVK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HVK_OK 0
+#define HVK_EINVAL 1
+#define HVK_EUNSUPPORTED 2
+#define HVK_EHIP 3
+
+int hvk_abi_version(void);
+const char* hvk_last_error_string(void);
+
+/* ---- Shifted-window cosine attention core ------------------------------------------
+ * Replaces swinv2.py:399-412 (roll + window_partition), 221-261 (WindowAttention core:
+ * normalize, q k^T, logit scale, CPB bias gather, shift mask, softmax, @v) and 420-429
+ * (window_reverse + roll back).  qkv: bf16 [B*H*W, 3C] = F.linear output of swinv2.py:220
+ * in UN-partitioned token order; out: bf16 [B*H*W, C] = input of proj (swinv2.py:262).
+ * bias_table: f32 [num_heads, (2w-1)^2] = 16*sigmoid(cpb_mlp(relative_coords_table))
+ * (swinv2.py:233-246 before the rpi gather); scale: f32 [num_heads] =
+ * exp(clamp(logit_scale, max=ln 100)) (swinv2.py:230).  window/shift are the clamped
+ * values of swinv2.py:328-331.  head_dim must be 32; window in {4, 6, 7, 8}. */
+int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale,
+                 int B, int H, int W, int C, int num_heads, int window, int shift,
+                 void* stream);
+size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
+/* dout: bf16 [B*H*W, C] (grad of `out`); dqkv: bf16 [B*H*W, 3C] (fully overwritten);
+ * dbias_table: f32 [num_heads, (2w-1)^2] (overwritten); dscale: f32 [num_heads]
+ * (overwritten, d loss / d scale). */
+int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bias_table,
+                 const float* scale, float* dbias_table, float* dscale, float* workspace,
+                 size_t workspace_bytes, int B, int H, int W, int C, int num_heads, int window,
+                 int shift, void* stream);
+
+/* ---- Post-norm residual LayerNorm --------------------------------------------------
+ * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a) (gamma, beta, eps)
+ * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(x))), and with x0 == NULL the
+ * plain norms of swinv2.py:494 (PatchMerging), 656 (patch_embed.norm), 833 (final norm).
+ * a: bf16 [rows, C]; x0: f32 [rows, C] or NULL; sample_scale: f32 [rows/rows_per_sample]
+ * or NULL (= 1; DropPath keep-mask / keep_prob); x_out: f32 [rows, C]; xb_out: bf16 copy
+ * of x_out or NULL; mean/rstd: f32 [rows] saved for the backward. */
+int hvk_ln_residual_fwd(const void* a, const float* x0, const float* gamma, const float* beta,
+                        const float* sample_scale, int rows, int C, int rows_per_sample,
+                        float eps, float* x_out, void* xb_out, float* mean, float* rstd,
+                        void* stream);
+/* gx: f32 [rows, C] or NULL, gxb: bf16 [rows, C] or NULL -- the two gradients of the
+ * output (f32 residual stream and its bf16 copy), summed.  gx0: f32 [rows, C] or NULL
+ * (gradient to the shortcut); ga: bf16 [rows, C]; dgamma/dbeta: f32 [C] (overwritten).
+ * workspace: f32, hvk_ln_bwd_workspace_bytes(C) bytes. */
+size_t hvk_ln_bwd_workspace_bytes(int C);
+int hvk_ln_residual_bwd(const void* a, const float* gamma, const float* sample_scale,
+                        const float* mean, const float* rstd, const float* gx, const void* gxb,
+                        int rows, int C, int rows_per_sample, float* gx0, void* ga,
+                        float* dgamma, float* dbeta, float* workspace, size_t workspace_bytes,
+                        void* stream);
+
+/* ---- PatchMerging 2x2 gather (swinv2.py:484-491) -----------------------------------
+ * out[b, (i, j), k*C + c] = x[b, (2i + dh_k, 2j + dw_k), c],
+ * (dh, dw)_k = (0,0), (1,0), (0,1), (1,1); x: bf16 [B, H*W, C], out: bf16 [B, H*W/4, 4C].
+ * scatter is the exact inverse (a permutation: every element written once). */
+int hvk_patch_merge_gather(const void* x, void* out, int B, int H, int W, int C, void* stream);
+int hvk_patch_merge_scatter(const void* gout, void* gx, int B, int H, int W, int C,
+                            void* stream);
+
+/* ---- Multitask / flat cross-entropy (hierarchy.py:65-94; models.py:112) -----------
+ * logits: f32 [B, ld]; head h occupies columns [head_off[h], head_off[h+1]).
+ * Targets: hard int64 [B, n_heads] (targets[b*n_heads + h]) or soft f32 [B, ld] (one of
+ * them non-NULL).  Forward writes row_loss f32 [n_heads, B] (per-row CE) and lse
+ * f32 [n_heads, B].  Backward: dlogits = grad_out * coeff[h] / B * (softmax*sum(t) - t). */
+int hvk_multitask_ce_fwd(const float* logits, int ld, int B, int n_heads, const int* head_off,
+                         const int64_t* targets, const float* soft, float* row_loss,
+                         float* lse, void* stream);
+int hvk_multitask_ce_bwd(const float* logits, int ld, int B, int n_heads, const int* head_off,
+                         const int64_t* targets, const float* soft, const float* lse,
+                         const float* coeff, const float* grad_out, float* dlogits,
+                         void* stream);
+
+/* ---- Hierarchical cross-entropy (HXE) --------------------------------------------
+ * Not implemented by the reference (hierarchy.py:183-185, models.py:105-106); knobs from
+ * configs.py:93-96.  Leaves are visited in `perm` order (NULL = identity) in which every
+ * taxonomy node owns a contiguous range: node n of tier t spans permuted positions
+ * [node_start[tier_base[t] + n], node_end[tier_base[t] + n]).  targets: int64 [B, 7] tier
+ * ids (tier 6 = leaf).  level_coeff f32 [8]: L_b = sum_l level_coeff[l] * LSE_l with
+ * LSE_l the log-sum-exp of logits over the target's level-l node (l = 0 leaf ... 6 top
+ * tier, 7 = all leaves).  Forward: row_loss f32 [B], lse f32 [B, 8].  Backward:
+ * dlogits = grad_out / B * sum_l level_coeff[l] * [k in node_l] * exp(z_k - LSE_l). */
+int hvk_hxe_fwd(const float* logits, int B, int L, const int* perm, const int64_t* targets,
+                const int* node_start, const int* node_end, const int* tier_base,
+                const float* level_coeff, float* row_loss, float* lse, void* stream);
+int hvk_hxe_bwd(const float* logits, int B, int L, const int* perm, const int64_t* targets,
+                const int* node_start, const int* node_end, const int* tier_base,
+                const float* level_coeff, const float* lse, const float* grad_out,
+                float* dlogits, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HVK_H_ */

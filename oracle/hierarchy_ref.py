@@ -156,3 +156,21 @@ def synthetic_inat_names(sizes=(3, 13, 51, 273, 1103, 4884, 10000)):
         parts = [f"{leaf:05d}"] + [f"t{t}n{ids[t]}" for t in range(N_TIERS)]
         names.append("_".join(parts))
     return names
+
+
+def hxe_loss_torch(logits, paths, perm, node_start, node_end, tier_base, lambdas):
+    """torch (autograd-capable, CPU) form of hxe_loss for the CPU baseline and
+    for gradient checks.  paths: [B, 7] tier ids; perm / node_* / tier_base as
+    in hvamd.hierarchy.Taxonomy (numpy)."""
+    import torch
+    z = logits[:, torch.as_tensor(perm, dtype=torch.long)]
+    total = logits.new_zeros(())
+    for b in range(z.shape[0]):
+        lse = []
+        for l in range(N_TIERS):
+            t = N_TIERS - 1 - l
+            k = tier_base[t] + int(paths[b, t])
+            lse.append(torch.logsumexp(z[b, node_start[k]:node_end[k]], dim=0))
+        lse.append(torch.logsumexp(z[b], dim=0))
+        total = total - sum(lambdas[l] * (lse[l] - lse[l + 1]) for l in range(N_TIERS))
+    return total / z.shape[0]

@@ -215,3 +215,30 @@ def state_shapes(img_size=224, patch_size=4, in_chans=3, embed_dim=96, depths=(2
         for i, n in enumerate(num_classes):
             s.update({f"head.heads.{i}.weight": (n, nf), f"head.heads.{i}.bias": (n,)})
     return s
+
+
+def wmsa_core_ref(qkv, bias_table, scale, H, W, heads, window, shift):
+    """Attention core from the qkv projection to the pre-proj output, on
+    UN-partitioned tokens: qkv [B, H*W, 3C] -> [B, H*W, C] (fp32, CPU).
+    Restates swinv2.py:221-261 with the roll/partition of 399-412 and the
+    reverse of 420-429.  bias_table [heads, (2w-1)^2] = 16*sigmoid(cpb);
+    scale [heads] = exp(clamp(logit_scale))."""
+    b, L, c3 = qkv.shape
+    c = c3 // 3
+    d = c // heads
+    g = torch.from_numpy(index_ref.window_gather_map(H, W, window, shift).astype(np.int64))
+    nw, n = g.shape
+    qw = qkv[:, g.reshape(-1)].reshape(b * nw, n, 3, heads, d)
+    q, k, v = (qw[:, :, i].transpose(1, 2) for i in range(3))
+    qn = q / q.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    kn = k / k.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+    s = (qn @ kn.transpose(-1, -2)) * scale.reshape(1, heads, 1, 1)
+    rpi = torch.from_numpy(index_ref.relative_position_index(window)).reshape(-1)
+    s = s + bias_table[:, rpi].reshape(1, heads, n, n)
+    m = index_ref.shift_mask(H, W, window, shift)
+    if m is not None:
+        s = (s.reshape(b, nw, heads, n, n) + torch.from_numpy(m)[None, :, None]).reshape(b * nw, heads, n, n)
+    o = (torch.softmax(s, dim=-1) @ v).transpose(1, 2).reshape(b, nw * n, c)
+    out = torch.empty(b, L, c, dtype=o.dtype)
+    out[:, g.reshape(-1)] = o
+    return out

@@ -1,0 +1,241 @@
+"""HIP path vs the reference's own outputs (golden fixtures) and the oracle, module by
+module and end to end.  Tolerance (north star): bf16 logits / losses within 1e-2 relative
+(relative L2 over the tensor); gradients within 2e-2..5e-2 relative L2."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hierarchy_ref, index_ref, swinv2_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(np.asarray(a, dtype=np.float64))
+    b = torch.as_tensor(np.asarray(b, dtype=np.float64))
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _load(m, seed):
+    shapes = {k: v.shape for k, v in m.state_dict().items()
+              if v.dtype.is_floating_point and not k.endswith("logit_clamp_max")
+              and "relative_coords_table" not in k and "attn_mask" not in k}
+    m.load_state_dict(swinv2_ref.init_params_from_rng(shapes, seed), strict=False)
+    return m.cuda()
+
+
+def _run(m, prefix, g, **kw):
+    x = torch.from_numpy(g[prefix + "x"]).cuda().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x, **kw)
+    y.float().backward(torch.from_numpy(g[prefix + "gy"]).cuda())
+    torch.cuda.synchronize()
+    return y, x
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_block_forward_backward_vs_reference(golden, shift):
+    from hvamd.swinv2 import SwinTransformerBlock
+    g = golden("module_golden")
+    pre = f"block_s{shift}."
+    m = _load(SwinTransformerBlock(dim=64, input_resolution=(14, 14), num_heads=2, window_size=7,
+                                   shift_size=shift), 20 + shift)
+    y, x = _run(m, pre, g)
+    assert rel(y.detach().float().cpu(), g[pre + "y"]) < 1e-2
+    assert rel(x.grad.float().cpu(), g[pre + "gx"]) < 2e-2
+    for k, p in m.named_parameters():
+        r = rel(p.grad.float().cpu(), g[pre + "grad." + k])
+        assert r < (5e-2 if "logit_scale" in k or "cpb_mlp" in k else 2e-2), (k, r)
+
+
+def test_block_window8_shifted_vs_reference(golden):
+    from hvamd.swinv2 import SwinTransformerBlock
+    g = golden("module_golden")
+    pre = "block_w8s4."
+    m = _load(SwinTransformerBlock(dim=64, input_resolution=(16, 16), num_heads=2, window_size=8,
+                                   shift_size=4), 40)
+    y, x = _run(m, pre, g)
+    assert rel(y.detach().float().cpu(), g[pre + "y"]) < 1e-2
+    assert rel(x.grad.float().cpu(), g[pre + "gx"]) < 2e-2
+
+
+@pytest.mark.parametrize("which,seed", [("wattn_mask.", 11), ("wattn_nomask.", 13)])
+def test_window_attention_reference_api(golden, which, seed):
+    """WindowAttention.forward(windows, mask) -- the reference's own call signature."""
+    from hvamd.swinv2 import SwinTransformerBlock
+    g = golden("module_golden")
+    blk = SwinTransformerBlock(dim=64, input_resolution=(14, 14), num_heads=2, window_size=7,
+                               shift_size=3)
+    wa = _load(blk.attn, seed)
+    mask = blk.attn_mask.cuda() if which == "wattn_mask." else None
+    y, x = _run(wa, which, g, mask=mask)
+    assert rel(y.detach().float().cpu(), g[which + "y"]) < 1e-2
+    assert rel(x.grad.float().cpu(), g[which + "gx"]) < 2e-2
+
+
+def test_patch_merging_vs_reference(golden):
+    from hvamd.swinv2 import PatchMerging
+    g = golden("module_golden")
+    m = _load(PatchMerging((14, 14), dim=32), 50)
+    y, x = _run(m, "merge.", g)
+    assert rel(y.detach().float().cpu(), g["merge.y"]) < 1e-2
+    assert rel(x.grad.float().cpu(), g["merge.gx"]) < 2e-2
+    assert rel(m.reduction.weight.grad.cpu(), g["merge.grad.reduction.weight"]) < 2e-2
+
+
+def test_patch_merge_gather_bit_exact():
+    import hvamd.ops as ops
+    B, H, W, C = 3, 28, 28, 48
+    x = torch.randn(B, H * W, C, device="cuda").bfloat16()
+    out = ops.patch_merge_gather(x, H, W)
+    idx = torch.from_numpy(index_ref.patch_merge_gather_map(H, W).astype(np.int64)).cuda()
+    ref = x[:, idx.reshape(-1)].reshape(B, -1, 4 * C)
+    assert torch.equal(out, ref)
+    xg = x.clone().requires_grad_(True)
+    ops.patch_merge_gather(xg, H, W).backward(out)
+    assert torch.equal(xg.grad, x)  # scatter is the exact inverse permutation
+
+
+@pytest.mark.parametrize("C", [96, 192, 384, 768, 1024, 64])
+def test_layernorm_residual_vs_torch(C):
+    import hvamd.ops as ops
+    B, L = 3, 50
+    a = torch.randn(B, L, C, device="cuda").bfloat16().requires_grad_(True)
+    x0 = torch.randn(B, L, C, device="cuda").requires_grad_(True)
+    gma = (1 + 0.1 * torch.randn(C, device="cuda")).requires_grad_(True)
+    bta = (0.1 * torch.randn(C, device="cuda")).requires_grad_(True)
+    s = torch.tensor([0.0, 1.25, 1.25], device="cuda")
+    x, xb = ops.layer_norm_residual(a, x0, gma, bta, s, L, 1e-5)
+    ref = x0 + s.view(B, 1, 1) * torch.nn.functional.layer_norm(a.float(), (C,), gma, bta, 1e-5)
+    assert rel(x.detach().cpu(), ref.detach().cpu()) < 1e-5
+    assert torch.equal(xb, x.detach().bfloat16())
+    gx = torch.randn_like(x)
+    gxb = torch.randn_like(x).bfloat16()
+    torch.autograd.backward([x, xb], [gx, gxb])
+    mine = [t.grad.float().clone() for t in (a, x0, gma, bta)]
+    for t in (a, x0, gma, bta):
+        t.grad = None
+    ref.backward(gx + gxb.float())
+    for m_, t in zip(mine, (a, x0, gma, bta)):
+        assert rel(m_.cpu(), t.grad.float().cpu()) < 1e-2
+
+
+MINI = dict(img_size=56, embed_dim=32, depths=[2, 2], num_heads=[1, 2], window_size=7,
+            drop_path_rate=0.0)
+TINY = dict(img_size=224, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+            window_size=7, drop_path_rate=0.0)
+
+
+def _model(cfg, nc):
+    from hvamd.swinv2 import SwinTransformerV2
+    net = SwinTransformerV2(num_classes=nc, **cfg)
+    shapes = {k: v.shape for k, v in net.state_dict().items()
+              if k.endswith(("weight", "bias", "logit_scale")) and "relative" not in k}
+    net.load_state_dict(swinv2_ref.init_params_from_rng(shapes, 7), strict=False)
+    return net.cuda()
+
+
+@pytest.mark.parametrize("name,cfg,nc", [("mini", MINI, 10), ("tiny", TINY, 1000),
+                                         ("mini_mt", MINI, (3, 4, 5, 6, 7, 8, 9))])
+def test_model_logits_vs_reference(golden, name, cfg, nc):
+    g = golden("model_golden")
+    net = _model(cfg, nc).eval()
+    x = torch.from_numpy(np.random.default_rng(42).standard_normal(
+        (2, 3, cfg["img_size"], cfg["img_size"])).astype(np.float32)).cuda()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = net(x)
+    if isinstance(y, list):
+        for i, a in enumerate(y):
+            assert rel(a.float().cpu(), g[f"{name}.logits{i}"]) < 1e-2
+    else:
+        r32 = rel(y.float().cpu(), g[f"{name}.logits"])
+        rbf = rel(y.float().cpu(), g[f"{name}.logits_bf16"])
+        assert r32 < 1e-2, (r32, rbf)
+
+
+def test_model_parameter_gradients_vs_reference(golden):
+    g = golden("model_golden")
+    net = _model(MINI, 10).train()
+    x = torch.from_numpy(np.random.default_rng(42).standard_normal((2, 3, 56, 56)).astype(np.float32))
+    x = x.cuda().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = net(x)
+    y.float().backward(torch.from_numpy(np.random.default_rng(43).standard_normal((2, 10)).astype(np.float32)).cuda())
+    torch.cuda.synchronize()
+    assert rel(x.grad.cpu(), g["mini.gx"]) < 3e-2
+    worst = {}
+    for k, p in net.named_parameters():
+        worst[k] = rel(p.grad.float().cpu(), g["mini.grad." + k])
+    bad = {k: v for k, v in worst.items() if v > (1e-1 if ("logit_scale" in k or "cpb" in k) else 5e-2)}
+    assert not bad, bad
+
+
+# ------------------------------------------------------------------ losses
+def test_multitask_ce_vs_reference(golden):
+    from hvamd.hierarchy import MultitaskCrossEntropy
+    from hvamd.algorithmic import smooth_labels
+    g = golden("loss_golden")
+    logits = [torch.from_numpy(g[f"mt.logits{i}"]).cuda().requires_grad_(True) for i in range(7)]
+    tgt = torch.from_numpy(g["mt.targets"]).cuda()
+    fn = MultitaskCrossEntropy(coeffs=list(g["mt.coeffs"])).cuda()
+    lh = fn(logits, tgt)
+    assert abs(lh.item() - float(g["mt.loss_hard"])) < 1e-5 * abs(float(g["mt.loss_hard"]))
+    soft = [smooth_labels(z, t, float(g["mt.smoothing"])) for z, t in zip(logits, tgt.T)]
+    ls = fn(logits, soft)
+    assert abs(ls.item() - float(g["mt.loss_soft"])) < 1e-5 * abs(float(g["mt.loss_soft"]))
+    ls.backward()
+    ref = [z.detach().cpu().clone().requires_grad_(True) for z in logits]
+    lr = sum(c * torch.nn.functional.cross_entropy(z, s.cpu())
+             for c, z, s in zip(list(g["mt.coeffs"]), ref, soft))
+    lr.backward()
+    for a, b in zip(logits, ref):
+        assert rel(a.grad.cpu(), b.grad) < 1e-4
+
+
+def test_flat_soft_cross_entropy_equals_torch():
+    from hvamd.hierarchy import soft_cross_entropy
+    z = torch.randn(64, 1000, device="cuda", requires_grad=True)
+    t = torch.randint(0, 1000, (64,), device="cuda")
+    l = soft_cross_entropy(z, t)
+    ref = torch.nn.functional.cross_entropy(z.detach().cpu(), t.cpu())
+    assert abs(l.item() - ref.item()) < 1e-5 * abs(ref.item())
+
+
+@pytest.mark.parametrize("weights", ["uniform", "exponential"])
+@pytest.mark.parametrize("sizes", [(2, 3, 4, 5, 6, 7, 12), (3, 13, 51, 273, 1103, 4884, 10000)])
+def test_hxe_vs_oracle(weights, sizes):
+    from hvamd.hierarchy import HierarchicalCrossEntropy, Taxonomy
+    tax = Taxonomy.synthetic(sizes)
+    rng = np.random.default_rng(0)
+    B = 16
+    z = (3 * rng.standard_normal((B, tax.num_leaves))).astype(np.float32)
+    leaves = rng.integers(0, tax.num_leaves, B)
+    lam = hierarchy_ref.hxe_level_weights(weights, 0.1)
+    ref = hierarchy_ref.hxe_loss(z, tax.leaf_paths, leaves, lam)
+    fn = HierarchicalCrossEntropy(tax, tree_weights=weights).cuda()
+    zt = torch.from_numpy(z).cuda().requires_grad_(True)
+    loss = fn(zt, torch.from_numpy(leaves).cuda())
+    assert abs(loss.item() - ref) < 1e-4 * max(1.0, abs(ref))
+    loss.backward()
+    zc = torch.from_numpy(z).double().requires_grad_(True)
+    hierarchy_ref.hxe_loss_torch(zc, tax.leaf_paths[leaves], tax.perm, tax.node_start,
+                                 tax.node_end, tax.tier_base, lam).backward()
+    assert rel(zt.grad.cpu(), zc.grad) < 1e-4
+
+
+def test_hxe_with_non_identity_leaf_order():
+    """Class numbers NOT in taxonomic order -> perm != identity, segments through perm."""
+    from hvamd.hierarchy import HierarchicalCrossEntropy, Taxonomy
+    names = hierarchy_ref.synthetic_inat_names((2, 3, 4, 5, 6, 7, 40))
+    rng = np.random.default_rng(1)
+    shuffled_ids = rng.permutation(len(names))
+    names = [f"{shuffled_ids[i]:05d}" + n[5:] for i, n in enumerate(names)]
+    tax = Taxonomy(names)
+    assert not tax.identity_perm
+    z = rng.standard_normal((8, tax.num_leaves)).astype(np.float32)
+    leaves = rng.integers(0, tax.num_leaves, 8)
+    lam = hierarchy_ref.hxe_level_weights("exponential", 0.1)
+    ref = hierarchy_ref.hxe_loss(z, tax.leaf_paths, leaves, lam)
+    fn = HierarchicalCrossEntropy(tax, tree_weights="exponential").cuda()
+    loss = fn(torch.from_numpy(z).cuda(), torch.from_numpy(tax.leaf_paths[leaves]).cuda())
+    assert abs(loss.item() - ref) < 1e-4 * max(1.0, abs(ref))
