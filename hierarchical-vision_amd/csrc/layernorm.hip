@@ -152,13 +152,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd p) {
   }
 }
 
-__global__ __launch_bounds__(256) void ln_bwd_reduce_kernel(const float* part, int nblk, int C,
-                                                            float* dgamma, float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// dgamma/dbeta = column sums of the per-block partials [nblk][2C]: one wave per
+// (64-column group, row group), 8 independent loads in flight, one atomic per column.
+constexpr int kRedRowGroups = 32;
+__global__ __launch_bounds__(64) void ln_bwd_reduce_kernel(const float* part, int nblk, int C,
+                                                           float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
   if (c >= 2 * C) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(size_t)b * 2 * C + c];
-  if (c < C) dgamma[c] = s; else dbeta[c - C] = s;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = blockIdx.y;
+  for (; b + 7 * kRedRowGroups < nblk; b += 8 * kRedRowGroups)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(b + u * kRedRowGroups) * 2 * C + c];
+  for (; b < nblk; b += kRedRowGroups) s[0] += part[(size_t)b * 2 * C + c];
+  const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  atomicAdd(c < C ? dgamma + c : dbeta + (c - C), t);
 }
 
 constexpr int kBwdBlocks = 1024;
@@ -213,8 +221,11 @@ int hvk_ln_residual_bwd(const void* a, const float* gamma, const float* sample_s
           static_cast<hvk_bf16*>(ga), workspace};
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, st, p);
   HVK_CHECK_LAUNCH("ln_bwd");
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, st,
-                     workspace, grid, C, dgamma, dbeta);
+  if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, st) != hipSuccess ||
+      hipMemsetAsync(dbeta, 0, sizeof(float) * C, st) != hipSuccess)
+    return hvk_set_error(HVK_EHIP, "hvk_ln_residual_bwd: memset failed");
+  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((2 * C + 63) / 64, kRedRowGroups), dim3(64), 0,
+                     st, workspace, grid, C, dgamma, dbeta);
   HVK_CHECK_LAUNCH("ln_bwd_reduce");
   return HVK_OK;
 }

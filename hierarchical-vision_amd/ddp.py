@@ -25,6 +25,12 @@ class GradientBuckets:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         params = [p for p in module.parameters() if p.requires_grad]
+        self.params = params
+        self.enabled = self.world > 1
+        self.buckets = []
+        self._hooks = []
+        if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
+            return
         limit = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets = []  # list of (flat buffer, [params])
         cur, size = [], 0
@@ -38,8 +44,6 @@ class GradientBuckets:
             self.buckets.append(self._make(cur, size))
         self._pending = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
-        self._hooks = []
-        self.enabled = self.world > 1
         for bi, (_, ps) in enumerate(self.buckets):
             for p in ps:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
@@ -68,6 +72,10 @@ class GradientBuckets:
 
     def reset(self):
         """Zero every bucket in place (grads stay views) before the next backward."""
+        if not self.enabled:
+            for p in self.params:
+                p.grad = None
+            return
         for i, (flat, ps) in enumerate(self.buckets):
             flat.zero_()
             self._pending[i] = len(ps)

@@ -5,6 +5,7 @@ current stream; tensors are plumbing (PyTorch owns the memory).  There is no
 eager/CPU fallback: a CPU tensor or a missing library raises.
 """
 import torch
+import torch.nn.functional as F
 
 from . import _lib
 from ._lib import call, ptr, stream
@@ -39,6 +40,58 @@ def _bf16(t):
 def _f32(t):
     t = t if t.dtype == torch.float32 else t.float()
     return t.contiguous()
+
+
+# --------------------------------------------------------------------------- Linear
+def _split_k_chunks(rows):
+    """Chunk count for the weight-gradient reduction over `rows` tokens: a power of two
+    dividing rows, chunks of >= 2048 rows, at most 256 chunks."""
+    nc = 1
+    while nc < 256 and rows % (2 * nc) == 0 and rows // (2 * nc) >= 2048:
+        nc *= 2
+    return nc
+
+
+def weight_grad(g, x):
+    """dW = g^T x in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to ~10^6) and
+    N, K small: the library picks ~50 workgroups for this shape, so split the token
+    reduction into a batched GEMM over chunks (thousands of workgroups) + a small sum."""
+    M = g.shape[0]
+    nc = _split_k_chunks(M)
+    if nc == 1:
+        return torch.mm(g.t(), x, out_dtype=torch.float32)
+    kc = M // nc
+    part = torch.bmm(g.view(nc, kc, -1).transpose(1, 2), x.view(nc, kc, -1),
+                     out_dtype=torch.float32)
+    return part.sum(dim=0)
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b with bf16 operands (f32 master W, b); backward returns f32 dW / db
+    directly (no bf16 round trip), dW via the split-token batched GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        xb = _bf16(x)
+        wb = weight.to(torch.bfloat16)
+        y = F.linear(xb, wb, bias.to(torch.bfloat16) if bias is not None else None)
+        ctx.save_for_backward(xb, wb)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        N, K = wb.shape
+        g2 = _bf16(gy).reshape(-1, N)
+        gx = (g2 @ wb).reshape(xb.shape) if ctx.needs_input_grad[0] else None
+        dw = weight_grad(g2, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
+        db = g2.sum(dim=0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, dw, db
+
+
+def linear(x, weight, bias=None):
+    return LinearFn.apply(x, weight, bias)
 
 
 # --------------------------------------------------------------------------- W-MSA

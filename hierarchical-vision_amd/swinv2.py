@@ -116,7 +116,8 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+        h = self.drop(self.act(ops.linear(x, self.fc1.weight, self.fc1.bias)))
+        return self.drop(ops.linear(h, self.fc2.weight, self.fc2.bias))
 
 
 class WindowAttention(nn.Module):
@@ -177,10 +178,10 @@ class WindowAttention(nn.Module):
 
     def forward_tokens(self, x, H, W, shift):
         """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] (after proj)."""
-        qkv = F.linear(x, self.qkv.weight, self.qkv_bias_vector())
+        qkv = ops.linear(x, self.qkv.weight, self.qkv_bias_vector())
         o = ops.window_attention_core(qkv, self.bias_table(), self.scales(), H, W, self.num_heads,
                                       self.window_size[0], shift)
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj.bias))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -289,7 +290,7 @@ class PatchMerging(nn.Module):
         assert L == H * W, "input feature has wrong size"
         assert H % 2 == 0 and W % 2 == 0, f"x size ({H}*{W}) are not even."
         xm = ops.patch_merge_gather(s.bf16, H, W)
-        y = F.linear(xm, self.reduction.weight)
+        y = ops.linear(xm, self.reduction.weight)
         x, xb = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1,
                                         self.norm.eps)
         return ResidualStream(x, xb)
@@ -381,7 +382,7 @@ class PatchEmbed(nn.Module):
         gh, gw = self.patches_resolution
         xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
         patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * ph * pw)
-        y = F.linear(patches, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
+        y = ops.linear(patches, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
         if self.norm is None:
             return _as_stream(y)
         x32, x16 = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1,

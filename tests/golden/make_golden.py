@@ -220,6 +220,15 @@ def main():
             models["mini.gx"] = xx.grad.numpy()
             for k, v in net.named_parameters():
                 models["mini.grad." + k] = v.grad.numpy()
+            # the same backward under CPU bf16 autocast: the reference's own bf16 error
+            net.zero_grad()
+            xx = x.clone().requires_grad_(True)
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                out = net(xx)
+            out.float().backward(g)
+            models["mini.gx_bf16"] = xx.grad.float().numpy()
+            for k, v in net.named_parameters():
+                models["mini.grad_bf16." + k] = v.grad.float().numpy()
     keys = list(ref.SwinTransformerV2(**cfgs["tiny"]).state_dict().keys())
     models["tiny.state_keys"] = np.array(keys)
     np.savez_compressed(os.path.join(HERE, "model_golden.npz"), **models)
