@@ -24,10 +24,13 @@ SIGNATURES = {
     "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
-    "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
+    "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),
-    "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
-                                 _sz, _p]),
+    "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
+                                 _p, _sz, _p]),
+    "hvk_bias_gelu_fwd": (_i, [_p, _p, _p, _i, _i, _p]),
+    "hvk_bias_gelu_bwd_workspace_bytes": (_sz, [_i]),
+    "hvk_bias_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _p, _sz, _i, _i, _p]),
     "hvk_patch_merge_gather": (_i, [_p, _p, _i, _i, _i, _i, _p]),
     "hvk_patch_merge_scatter": (_i, [_p, _p, _i, _i, _i, _i, _p]),
     "hvk_multitask_ce_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),

@@ -1,181 +1,263 @@
 // Post-norm residual LayerNorm for SwinV2's res-post-norm blocks (gfx950).
 //
-//   x = x0 + s[b] * (gamma * (a - mean) * rstd + beta)
+//   a' = a + abias                       (bias of the Linear that produced a, folded in)
+//   x  = x0 + s[b] * (gamma * (a' - mean) * rstd + beta)
 //
 // replaces `shortcut + drop_path(norm1(x))` / `x + drop_path(norm2(mlp(x)))`
-// (swinv2.py:431, 434) -- a is the bf16 output of the proj / fc2 GEMM, x0 the f32
-// residual stream, s the per-sample DropPath factor -- and, with no x0, the plain
-// norms of PatchMerging (swinv2.py:494), PatchEmbed (656) and the final norm (833).
-// It writes the f32 residual stream and its bf16 copy (the next GEMM's operand) in
-// one pass.  One wave per row; each lane owns bf16 pairs (4-byte loads) strided by 64.
+// (swinv2.py:431, 434) -- a is the bf16 output of the proj / fc2 GEMM (run without its
+// bias), x0 the f32 residual stream, s the per-sample DropPath factor -- and, with no x0,
+// the plain norms of PatchMerging (swinv2.py:494), PatchEmbed (656) and the final norm
+// (833).  One pass writes the f32 residual stream and its bf16 copy (next GEMM operand).
+// The backward also column-sums the branch gradient, which IS the folded bias's gradient,
+// so no separate bias-reduction pass exists.
+//
+// Layout: a row of C channels is owned by TPR lanes (power of two) holding EPT contiguous
+// channels each (16/32-byte bf16 loads, 32/64-byte f32 loads); a wave works on 64/TPR
+// rows at once, grid-strided.  Row statistics are TPR-lane xor-shuffle reductions.
 #include "hvk_common.h"
 
 namespace {
 
-constexpr int kRowsPerBlock = 4;  // one wave per row
-constexpr int kMaxPairs = 8;      // C <= 1024
+constexpr int kWaves = 4;
+
+template <int EPT>
+__device__ __forceinline__ void load_bf16(const hvk_bf16* p, float v[EPT]) {
+#pragma unroll
+  for (int i = 0; i < EPT / 8; ++i) {
+    const uint4 w = reinterpret_cast<const uint4*>(p)[i];
+    float f[8];
+    hvk_unpack8(w, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[8 * i + j] = f[j];
+  }
+}
+template <int EPT>
+__device__ __forceinline__ void store_bf16(hvk_bf16* p, const float v[EPT]) {
+#pragma unroll
+  for (int i = 0; i < EPT / 8; ++i) reinterpret_cast<uint4*>(p)[i] = hvk_pack8(v + 8 * i);
+}
+template <int EPT>
+__device__ __forceinline__ void load_f32(const float* p, float v[EPT]) {
+#pragma unroll
+  for (int i = 0; i < EPT / 4; ++i) {
+    const float4 w = reinterpret_cast<const float4*>(p)[i];
+    v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
+  }
+}
+template <int EPT>
+__device__ __forceinline__ void store_f32(float* p, const float v[EPT]) {
+#pragma unroll
+  for (int i = 0; i < EPT / 4; ++i)
+    reinterpret_cast<float4*>(p)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+template <int TPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = TPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
 
 struct LnFwd {
-  const hvk_bf16* a; const float* x0; const float* gamma; const float* beta; const float* sscale;
-  int rows, C, rows_per_sample; float eps;
+  const hvk_bf16* a; const float* abias; const float* x0; const float* gamma; const float* beta;
+  const float* sscale; int rows, C, rows_per_sample; float eps;
   float* x; hvk_bf16* xb; float* mean; float* rstd;
 };
 
-__global__ __launch_bounds__(256) void ln_fwd_kernel(LnFwd p) {
-  const int lane = threadIdx.x & 63;
-  const int npair = p.C >> 1;
-  for (int row = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); row < p.rows;
-       row += gridDim.x * kRowsPerBlock) {
-    const uint32_t* ar = reinterpret_cast<const uint32_t*>(p.a + (size_t)row * p.C);
-    float v[kMaxPairs][2];
+template <int EPT, int TPR>
+__global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
+  constexpr int RPW = 64 / TPR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / TPR, t = lane % TPR;
+  const int c0 = t * EPT;
+  const bool act = c0 < p.C;
+  float gm[EPT], bt[EPT], ab[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) { gm[j] = 0.f; bt[j] = 0.f; ab[j] = 0.f; }
+  if (act) {
+    load_f32<EPT>(p.gamma + c0, gm);
+    load_f32<EPT>(p.beta + c0, bt);
+    if (p.abias) load_f32<EPT>(p.abias + c0, ab);
+  }
+  const float invC = 1.f / p.C;
+  for (int row = (blockIdx.x * kWaves + wave) * RPW + sub; row < p.rows;
+       row += gridDim.x * kWaves * RPW) {
+    float v[EPT];
     float s = 0.f;
+    if (act) {
+      load_bf16<EPT>(p.a + (size_t)row * p.C + c0, v);
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-      const int j = lane + 64 * k;
-      if (j < npair) {
-        const uint32_t w = ar[j];
-        v[k][0] = hvk_lo(w); v[k][1] = hvk_hi(w);
-        s += v[k][0] + v[k][1];
-      } else {
-        v[k][0] = v[k][1] = 0.f;
-      }
+      for (int j = 0; j < EPT; ++j) { v[j] += ab[j]; s += v[j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) v[j] = 0.f;
     }
-    const float mu = hvk_wave_sum(s) / p.C;
+    const float mu = group_sum<TPR>(s) * invC;
     float ss = 0.f;
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-      const int j = lane + 64 * k;
-      if (j < npair) {
-        const float d0 = v[k][0] - mu, d1 = v[k][1] - mu;
-        ss += d0 * d0 + d1 * d1;
-      }
+      for (int j = 0; j < EPT; ++j) { const float d = v[j] - mu; ss += d * d; }
     }
-    const float var = hvk_wave_sum(ss) / p.C;
-    const float rs = rsqrtf(var + p.eps);
-    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-    const float2* x0r = p.x0 ? reinterpret_cast<const float2*>(p.x0 + (size_t)row * p.C) : nullptr;
-    float2* xr = reinterpret_cast<float2*>(p.x + (size_t)row * p.C);
-    uint32_t* xbr = p.xb ? reinterpret_cast<uint32_t*>(p.xb + (size_t)row * p.C) : nullptr;
-    const float2* g2 = reinterpret_cast<const float2*>(p.gamma);
-    const float2* b2 = reinterpret_cast<const float2*>(p.beta);
+    const float rs = rsqrtf(group_sum<TPR>(ss) * invC + p.eps);
+    if (act) {
+      const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
+      float r[EPT];
+      if (p.x0) load_f32<EPT>(p.x0 + (size_t)row * p.C + c0, r);
+      else {
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-      const int j = lane + 64 * k;
-      if (j < npair) {
-        const float2 gg = g2[j], bb = b2[j];
-        float y0 = ((v[k][0] - mu) * rs * gg.x + bb.x) * sc;
-        float y1 = ((v[k][1] - mu) * rs * gg.y + bb.y) * sc;
-        if (x0r) {
-          const float2 r = x0r[j];
-          y0 += r.x; y1 += r.y;
-        }
-        xr[j] = make_float2(y0, y1);
-        if (xbr) xbr[j] = hvk_pack2(y0, y1);
+        for (int j = 0; j < EPT; ++j) r[j] = 0.f;
       }
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) r[j] += ((v[j] - mu) * rs * gm[j] + bt[j]) * sc;
+      store_f32<EPT>(p.x + (size_t)row * p.C + c0, r);
+      if (p.xb) store_bf16<EPT>(p.xb + (size_t)row * p.C + c0, r);
+      if (t == 0) { p.mean[row] = mu; p.rstd[row] = rs; }
     }
-    if (lane == 0) { p.mean[row] = mu; p.rstd[row] = rs; }
   }
 }
 
 struct LnBwd {
-  const hvk_bf16* a; const float* gamma; const float* sscale; const float* mean; const float* rstd;
-  const float* gx; const hvk_bf16* gxb; int rows, C, rows_per_sample;
-  float* gx0; hvk_bf16* ga; float* part;  // part: [gridDim.x][2][C] per-block dgamma/dbeta
+  const hvk_bf16* a; const float* abias; const float* gamma; const float* sscale;
+  const float* mean; const float* rstd; const float* gx; const hvk_bf16* gxb;
+  int rows, C, rows_per_sample;
+  float* gx0; hvk_bf16* ga; float* part;  // part: [gridDim.x][3][C] dgamma / dbeta / dabias
 };
 
-__global__ __launch_bounds__(256) void ln_bwd_kernel(LnBwd p) {
-  __shared__ float red[2][kRowsPerBlock][2 * 64 * kMaxPairs];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int npair = p.C >> 1;
-  float dg[kMaxPairs][2], db[kMaxPairs][2];
+template <int EPT, int TPR>
+__global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
+  constexpr int RPW = 64 / TPR;
+  __shared__ float red[kWaves][3][TPR * EPT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / TPR, t = lane % TPR;
+  const int c0 = t * EPT;
+  const bool act = c0 < p.C;
+  float gm[EPT], ab[EPT], dg[EPT], db[EPT], dab[EPT];
 #pragma unroll
-  for (int k = 0; k < kMaxPairs; ++k) dg[k][0] = dg[k][1] = db[k][0] = db[k][1] = 0.f;
-  const float2* g2 = reinterpret_cast<const float2*>(p.gamma);
-  for (int row = blockIdx.x * kRowsPerBlock + wv; row < p.rows; row += gridDim.x * kRowsPerBlock) {
+  for (int j = 0; j < EPT; ++j) { gm[j] = ab[j] = dg[j] = db[j] = dab[j] = 0.f; }
+  if (act) {
+    load_f32<EPT>(p.gamma + c0, gm);
+    if (p.abias) load_f32<EPT>(p.abias + c0, ab);
+  }
+  const float invC = 1.f / p.C;
+  for (int row = (blockIdx.x * kWaves + wave) * RPW + sub; row < p.rows;
+       row += gridDim.x * kWaves * RPW) {
+    float y[EPT], go[EPT], gy[EPT];
+    float s1 = 0.f, s2 = 0.f;
     const float mu = p.mean[row], rs = p.rstd[row];
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-    const uint32_t* ar = reinterpret_cast<const uint32_t*>(p.a + (size_t)row * p.C);
-    const float2* gxr = p.gx ? reinterpret_cast<const float2*>(p.gx + (size_t)row * p.C) : nullptr;
-    const uint32_t* gxbr = p.gxb ? reinterpret_cast<const uint32_t*>(p.gxb + (size_t)row * p.C) : nullptr;
-    float y[kMaxPairs][2], gy[kMaxPairs][2], go[kMaxPairs][2];
-    float s1 = 0.f, s2 = 0.f;
+    if (act) {
+      load_bf16<EPT>(p.a + (size_t)row * p.C + c0, y);
+      if (p.gx) load_f32<EPT>(p.gx + (size_t)row * p.C + c0, go);
+      else {
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-      const int j = lane + 64 * k;
-      y[k][0] = y[k][1] = gy[k][0] = gy[k][1] = go[k][0] = go[k][1] = 0.f;
-      if (j < npair) {
-        const uint32_t w = ar[j];
-        y[k][0] = (hvk_lo(w) - mu) * rs;
-        y[k][1] = (hvk_hi(w) - mu) * rs;
-        float t0 = 0.f, t1 = 0.f;
-        if (gxr) { const float2 q = gxr[j]; t0 += q.x; t1 += q.y; }
-        if (gxbr) { const uint32_t q = gxbr[j]; t0 += hvk_lo(q); t1 += hvk_hi(q); }
-        go[k][0] = t0; go[k][1] = t1;       // gradient of the block output (and of x0)
-        const float o0 = t0 * sc, o1 = t1 * sc;  // gradient of the LN output
-        dg[k][0] += o0 * y[k][0]; dg[k][1] += o1 * y[k][1];
-        db[k][0] += o0; db[k][1] += o1;
-        const float2 gg = g2[j];
-        gy[k][0] = o0 * gg.x; gy[k][1] = o1 * gg.y;
-        s1 += gy[k][0] + gy[k][1];
-        s2 += gy[k][0] * y[k][0] + gy[k][1] * y[k][1];
+        for (int j = 0; j < EPT; ++j) go[j] = 0.f;
       }
+      if (p.gxb) {
+        float q[EPT];
+        load_bf16<EPT>(p.gxb + (size_t)row * p.C + c0, q);
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) go[j] += q[j];
+      }
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) {
+        y[j] = (y[j] + ab[j] - mu) * rs;
+        const float o = go[j] * sc;  // gradient of the LN output
+        dg[j] += o * y[j];
+        db[j] += o;
+        gy[j] = o * gm[j];
+        s1 += gy[j];
+        s2 += gy[j] * y[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) y[j] = go[j] = gy[j] = 0.f;
     }
-    s1 = hvk_wave_sum(s1) / p.C;
-    s2 = hvk_wave_sum(s2) / p.C;
-    uint32_t* gar = reinterpret_cast<uint32_t*>(p.ga + (size_t)row * p.C);
-    float2* gx0r = p.gx0 ? reinterpret_cast<float2*>(p.gx0 + (size_t)row * p.C) : nullptr;
+    s1 = group_sum<TPR>(s1) * invC;
+    s2 = group_sum<TPR>(s2) * invC;
+    if (act) {
+      float d[EPT];
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-      const int j = lane + 64 * k;
-      if (j < npair) {
-        const float d0 = rs * (gy[k][0] - s1 - y[k][0] * s2);
-        const float d1 = rs * (gy[k][1] - s1 - y[k][1] * s2);
-        gar[j] = hvk_pack2(d0, d1);
-        if (gx0r) gx0r[j] = make_float2(go[k][0], go[k][1]);
+      for (int j = 0; j < EPT; ++j) {
+        d[j] = rs * (gy[j] - s1 - y[j] * s2);
+        dab[j] += d[j];
       }
+      store_bf16<EPT>(p.ga + (size_t)row * p.C + c0, d);
+      if (p.gx0) store_f32<EPT>(p.gx0 + (size_t)row * p.C + c0, go);
     }
   }
-  // block partials of dgamma / dbeta (deterministic: no atomics)
+  // fold the RPW row slots of the wave (lanes t, t+TPR, ...), then the waves via LDS
 #pragma unroll
-  for (int k = 0; k < kMaxPairs; ++k) {
-    const int j = lane + 64 * k;
-    red[0][wv][2 * j] = dg[k][0]; red[0][wv][2 * j + 1] = dg[k][1];
-    red[1][wv][2 * j] = db[k][0]; red[1][wv][2 * j + 1] = db[k][1];
+  for (int m = TPR; m < 64; m <<= 1)
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      dg[j] += __shfl_xor(dg[j], m);
+      db[j] += __shfl_xor(db[j], m);
+      dab[j] += __shfl_xor(dab[j], m);
+    }
+  if (sub == 0) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      red[wave][0][c0 + j] = dg[j];
+      red[wave][1][c0 + j] = db[j];
+      red[wave][2][c0 + j] = dab[j];
+    }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < p.C; c += blockDim.x) {
-    float a0 = 0.f, a1 = 0.f;
+  for (int c = threadIdx.x; c < 3 * p.C; c += blockDim.x) {
+    const int k = c / p.C, cc = c % p.C;
+    float acc = 0.f;
 #pragma unroll
-    for (int w = 0; w < kRowsPerBlock; ++w) { a0 += red[0][w][c]; a1 += red[1][w][c]; }
-    p.part[(size_t)blockIdx.x * 2 * p.C + c] = a0;
-    p.part[(size_t)blockIdx.x * 2 * p.C + p.C + c] = a1;
+    for (int w = 0; w < kWaves; ++w) acc += red[w][k][cc];
+    p.part[(size_t)blockIdx.x * 3 * p.C + c] = acc;
   }
 }
 
-// dgamma/dbeta = column sums of the per-block partials [nblk][2C]: one wave per
-// (64-column group, row group), 8 independent loads in flight, one atomic per column.
+// column sums of the per-block partials [nblk][ncol]: one wave per (64-column group,
+// row group), 8 independent loads in flight, one atomic per column and row group.
 constexpr int kRedRowGroups = 32;
-__global__ __launch_bounds__(64) void ln_bwd_reduce_kernel(const float* part, int nblk, int C,
-                                                           float* dgamma, float* dbeta) {
+__global__ __launch_bounds__(64) void colsum_kernel(const float* part, int nblk, int ncol,
+                                                    float* out0, float* out1, float* out2, int C) {
   const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= 2 * C) return;
+  if (c >= ncol) return;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int b = blockIdx.y;
   for (; b + 7 * kRedRowGroups < nblk; b += 8 * kRedRowGroups)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(b + u * kRedRowGroups) * 2 * C + c];
-  for (; b < nblk; b += kRedRowGroups) s[0] += part[(size_t)b * 2 * C + c];
-  const float t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  atomicAdd(c < C ? dgamma + c : dbeta + (c - C), t);
+    for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(b + u * kRedRowGroups) * ncol + c];
+  for (; b < nblk; b += kRedRowGroups) s[0] += part[(size_t)b * ncol + c];
+  const float v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  float* dst = c < C ? out0 + c : (c < 2 * C ? out1 + (c - C) : out2 + (c - 2 * C));
+  if (dst) atomicAdd(dst, v);
 }
 
 constexpr int kBwdBlocks = 1024;
 
-int check_shape(const char* who, int rows, int C, int rps) {
+// (EPT, TPR) for a channel count: TPR * EPT >= C, TPR a power of two <= 64
+int pick_layout(int C, int& ept, int& tpr) {
+  if (C % 8) return 1;
+  ept = C > 512 ? 16 : 8;
+  tpr = 1;
+  while (tpr * ept < C) tpr <<= 1;
+  return tpr > 64 ? 1 : 0;
+}
+
+#define HVK_LN_DISPATCH(KERNEL, GRID, ST, ARGS)                                               \
+  switch (ept * 1000 + tpr) {                                                                 \
+    case 8001: hipLaunchKernelGGL((KERNEL<8, 1>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;   \
+    case 8002: hipLaunchKernelGGL((KERNEL<8, 2>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;   \
+    case 8004: hipLaunchKernelGGL((KERNEL<8, 4>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;   \
+    case 8008: hipLaunchKernelGGL((KERNEL<8, 8>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;   \
+    case 8016: hipLaunchKernelGGL((KERNEL<8, 16>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
+    case 8032: hipLaunchKernelGGL((KERNEL<8, 32>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
+    case 8064: hipLaunchKernelGGL((KERNEL<8, 64>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
+    case 16064: hipLaunchKernelGGL((KERNEL<16, 64>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break; \
+    default: return hvk_set_error(HVK_EUNSUPPORTED, "layernorm: no layout for C=%d", C);      \
+  }
+
+int check_shape(const char* who, int rows, int C, int rps, int& ept, int& tpr) {
   if (rows <= 0 || C <= 0 || rps <= 0)
     return hvk_set_error(HVK_EINVAL, "%s: bad shape rows=%d C=%d rows_per_sample=%d", who, rows, C, rps);
-  if (C % 2 || C > 2 * 64 * kMaxPairs)
-    return hvk_set_error(HVK_EUNSUPPORTED, "%s: C=%d must be even and <= %d", who, C, 2 * 64 * kMaxPairs);
+  if (pick_layout(C, ept, tpr))
+    return hvk_set_error(HVK_EUNSUPPORTED, "%s: C=%d must be a multiple of 8 and <= 1024", who, C);
   return HVK_OK;
 }
 
@@ -183,50 +265,56 @@ int check_shape(const char* who, int rows, int C, int rps) {
 
 extern "C" {
 
-int hvk_ln_residual_fwd(const void* a, const float* x0, const float* gamma, const float* beta,
-                        const float* sample_scale, int rows, int C, int rows_per_sample,
-                        float eps, float* x_out, void* xb_out, float* mean, float* rstd,
-                        void* stream) {
-  int rc = check_shape("hvk_ln_residual_fwd", rows, C, rows_per_sample);
+int hvk_ln_residual_fwd(const void* a, const float* abias, const float* x0, const float* gamma,
+                        const float* beta, const float* sample_scale, int rows, int C,
+                        int rows_per_sample, float eps, float* x_out, void* xb_out, float* mean,
+                        float* rstd, void* stream) {
+  int ept, tpr;
+  int rc = check_shape("hvk_ln_residual_fwd", rows, C, rows_per_sample, ept, tpr);
   if (rc) return rc;
   if (!a || !gamma || !beta || !x_out || !mean || !rstd)
     return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_fwd: null pointer");
-  LnFwd p{static_cast<const hvk_bf16*>(a), x0, gamma, beta, sample_scale, rows, C,
+  LnFwd p{static_cast<const hvk_bf16*>(a), abias, x0, gamma, beta, sample_scale, rows, C,
           rows_per_sample, eps, x_out, static_cast<hvk_bf16*>(xb_out), mean, rstd};
-  int grid = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-  if (grid > 256 * 32) grid = 256 * 32;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream), p);
+  const int rows_per_block = kWaves * (64 / tpr);
+  int grid = (rows + rows_per_block - 1) / rows_per_block;
+  if (grid > 256 * 8) grid = 256 * 8;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HVK_LN_DISPATCH(ln_fwd_kernel, dim3(grid), st, p);
   HVK_CHECK_LAUNCH("ln_fwd");
   return HVK_OK;
 }
 
-size_t hvk_ln_bwd_workspace_bytes(int C) { return (size_t)kBwdBlocks * 2 * C * sizeof(float); }
+size_t hvk_ln_bwd_workspace_bytes(int C) { return (size_t)kBwdBlocks * 3 * C * sizeof(float); }
 
-int hvk_ln_residual_bwd(const void* a, const float* gamma, const float* sample_scale,
-                        const float* mean, const float* rstd, const float* gx, const void* gxb,
-                        int rows, int C, int rows_per_sample, float* gx0, void* ga,
-                        float* dgamma, float* dbeta, float* workspace, size_t workspace_bytes,
-                        void* stream) {
-  int rc = check_shape("hvk_ln_residual_bwd", rows, C, rows_per_sample);
+int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
+                        const float* sample_scale, const float* mean, const float* rstd,
+                        const float* gx, const void* gxb, int rows, int C, int rows_per_sample,
+                        float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
+                        float* workspace, size_t workspace_bytes, void* stream) {
+  int ept, tpr;
+  int rc = check_shape("hvk_ln_residual_bwd", rows, C, rows_per_sample, ept, tpr);
   if (rc) return rc;
   if (!a || !gamma || !mean || !rstd || !ga || !dgamma || !dbeta || !workspace || (!gx && !gxb))
     return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd: null pointer");
   if (workspace_bytes < hvk_ln_bwd_workspace_bytes(C))
     return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  int grid = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+  const int rows_per_block = kWaves * (64 / tpr);
+  int grid = (rows + rows_per_block - 1) / rows_per_block;
   if (grid > kBwdBlocks) grid = kBwdBlocks;
-  LnBwd p{static_cast<const hvk_bf16*>(a), gamma, sample_scale, mean, rstd, gx,
+  LnBwd p{static_cast<const hvk_bf16*>(a), abias, gamma, sample_scale, mean, rstd, gx,
           static_cast<const hvk_bf16*>(gxb), rows, C, rows_per_sample, gx0,
           static_cast<hvk_bf16*>(ga), workspace};
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(grid), dim3(256), 0, st, p);
+  HVK_LN_DISPATCH(ln_bwd_kernel, dim3(grid), st, p);
   HVK_CHECK_LAUNCH("ln_bwd");
   if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, st) != hipSuccess ||
-      hipMemsetAsync(dbeta, 0, sizeof(float) * C, st) != hipSuccess)
+      hipMemsetAsync(dbeta, 0, sizeof(float) * C, st) != hipSuccess ||
+      (dabias && hipMemsetAsync(dabias, 0, sizeof(float) * C, st) != hipSuccess))
     return hvk_set_error(HVK_EHIP, "hvk_ln_residual_bwd: memset failed");
-  hipLaunchKernelGGL(ln_bwd_reduce_kernel, dim3((2 * C + 63) / 64, kRedRowGroups), dim3(64), 0,
-                     st, workspace, grid, C, dgamma, dbeta);
-  HVK_CHECK_LAUNCH("ln_bwd_reduce");
+  hipLaunchKernelGGL(colsum_kernel, dim3((3 * C + 63) / 64, kRedRowGroups), dim3(64), 0, st,
+                     workspace, grid, 3 * C, dgamma, dbeta, dabias, C);
+  HVK_CHECK_LAUNCH("ln_bwd_colsum");
   return HVK_OK;
 }
 

@@ -1,0 +1,147 @@
+// Fused bias + exact GELU of the SwinV2 MLP (swinv2.py:60-62: fc1 -> GELU) on gfx950.
+//
+// fc1 runs as a plain GEMM without its bias; this kernel applies `u = h + b`,
+// `y = 0.5 u (1 + erf(u / sqrt 2))` and writes bf16.  The backward recomputes u from the
+// saved GEMM output and, in the same pass, column-sums the pre-activation gradient --
+// that sum is the fc1 bias gradient, so no separate reduction reads it again.
+//
+// Layout: a wave owns 64 consecutive 8-channel chunks (512 channels) of a row tile and
+// walks rows; each lane keeps its 8 column sums in registers.
+#include "hvk_common.h"
+
+namespace {
+
+constexpr int kWaves = 4;
+constexpr float kInvSqrt2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erff(u * kInvSqrt2)); }
+__device__ __forceinline__ float gelu_grad(float u) {
+  return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+}
+
+__global__ __launch_bounds__(64 * kWaves) void bias_gelu_fwd_kernel(const hvk_bf16* __restrict__ h,
+                                                                    const float* __restrict__ b,
+                                                                    hvk_bf16* __restrict__ y,
+                                                                    int rows, int N) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 8;
+  if (c >= N) return;
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bb[j] = b ? b[c + j] : 0.f;
+  for (int r = blockIdx.x * kWaves + wave; r < rows; r += gridDim.x * kWaves) {
+    const size_t off = (size_t)r * N + c;
+    float f[8];
+    hvk_unpack8(*reinterpret_cast<const uint4*>(h + off), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = gelu(f[j] + bb[j]);
+    *reinterpret_cast<uint4*>(y + off) = hvk_pack8(f);
+  }
+}
+
+__global__ __launch_bounds__(64 * kWaves) void bias_gelu_bwd_kernel(const hvk_bf16* __restrict__ h,
+                                                                    const float* __restrict__ b,
+                                                                    const hvk_bf16* __restrict__ gy,
+                                                                    hvk_bf16* __restrict__ gh,
+                                                                    float* __restrict__ part,
+                                                                    int rows, int N) {
+  __shared__ float red[kWaves][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 8;
+  const bool act = c < N;
+  float bb[8], acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { bb[j] = (act && b) ? b[c + j] : 0.f; acc[j] = 0.f; }
+  if (act) {
+    for (int r = blockIdx.x * kWaves + wave; r < rows; r += gridDim.x * kWaves) {
+      const size_t off = (size_t)r * N + c;
+      float u[8], g[8];
+      hvk_unpack8(*reinterpret_cast<const uint4*>(h + off), u);
+      hvk_unpack8(*reinterpret_cast<const uint4*>(gy + off), g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[j] *= gelu_grad(u[j] + bb[j]);
+        acc[j] += g[j];
+      }
+      *reinterpret_cast<uint4*>(gh + off) = hvk_pack8(g);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += blockDim.x) {
+    const int cc = blockIdx.y * 512 + i;
+    if (cc < N) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += red[w][i];
+      part[(size_t)blockIdx.x * N + cc] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void colsum_rows_kernel(const float* part, int nblk, int N,
+                                                         float* out) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= N) return;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int b = blockIdx.y;
+  const int G = gridDim.y;
+  for (; b + 7 * G < nblk; b += 8 * G)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(b + u * G) * N + c];
+  for (; b < nblk; b += G) s[0] += part[(size_t)b * N + c];
+  atomicAdd(out + c, ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])));
+}
+
+constexpr int kBwdRowBlocks = 512;
+
+}  // namespace
+
+extern "C" {
+
+size_t hvk_bias_gelu_bwd_workspace_bytes(int N) {
+  return (size_t)kBwdRowBlocks * N * sizeof(float);
+}
+
+int hvk_bias_gelu_fwd(const void* h, const float* bias, void* y, int rows, int N, void* stream) {
+  if (!h || !y) return hvk_set_error(HVK_EINVAL, "hvk_bias_gelu_fwd: null pointer");
+  if (rows <= 0 || N <= 0 || N % 8)
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_bias_gelu_fwd: rows=%d N=%d (N %% 8 == 0)", rows, N);
+  int gx = (rows + kWaves - 1) / kWaves;
+  if (gx > 2048) gx = 2048;
+  dim3 grid(gx, (N + 511) / 512);
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, grid, dim3(64 * kWaves), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const hvk_bf16*>(h), bias,
+                     static_cast<hvk_bf16*>(y), rows, N);
+  HVK_CHECK_LAUNCH("bias_gelu_fwd");
+  return HVK_OK;
+}
+
+int hvk_bias_gelu_bwd(const void* h, const float* bias, const void* gy, void* gh, float* dbias,
+                      float* workspace, size_t workspace_bytes, int rows, int N, void* stream) {
+  if (!h || !gy || !gh) return hvk_set_error(HVK_EINVAL, "hvk_bias_gelu_bwd: null pointer");
+  if (rows <= 0 || N <= 0 || N % 8)
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_bias_gelu_bwd: rows=%d N=%d", rows, N);
+  if (dbias && (!workspace || workspace_bytes < hvk_bias_gelu_bwd_workspace_bytes(N)))
+    return hvk_set_error(HVK_EINVAL, "hvk_bias_gelu_bwd: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  int gx = (rows + kWaves - 1) / kWaves;
+  if (gx > kBwdRowBlocks) gx = kBwdRowBlocks;
+  dim3 grid(gx, (N + 511) / 512);
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, grid, dim3(64 * kWaves), 0, st,
+                     static_cast<const hvk_bf16*>(h), bias, static_cast<const hvk_bf16*>(gy),
+                     static_cast<hvk_bf16*>(gh), workspace, rows, N);
+  HVK_CHECK_LAUNCH("bias_gelu_bwd");
+  if (dbias) {
+    if (hipMemsetAsync(dbias, 0, sizeof(float) * N, st) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_bias_gelu_bwd: memset failed");
+    hipLaunchKernelGGL(colsum_rows_kernel, dim3((N + 63) / 64, 16), dim3(64), 0, st, workspace,
+                       gx, N, dbias);
+    HVK_CHECK_LAUNCH("bias_gelu_colsum");
+  }
+  return HVK_OK;
+}
+
+}  // extern "C"

@@ -141,53 +141,89 @@ def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift
 
 # --------------------------------------------------------------------------- LayerNorm
 class LayerNormResidual(torch.autograd.Function):
-    """x = x0 + s[b] * LayerNorm(a); returns (x f32, x bf16 copy)."""
+    """x = x0 + s[b] * LayerNorm(a + abias); returns (x f32, x bf16 copy).  abias is the
+    bias of the Linear that produced `a` (that GEMM runs without it)."""
 
     @staticmethod
-    def forward(ctx, a, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+    def forward(ctx, a, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
         C = a.shape[-1]
         rows = a.numel() // C
         a = _bf16(a)
         gamma, beta = _f32(gamma), _f32(beta)
-        if x0 is not None:
-            x0 = _f32(x0)
-        if sample_scale is not None:
-            sample_scale = _f32(sample_scale)
+        abias = _f32(abias) if abias is not None else None
+        x0 = _f32(x0) if x0 is not None else None
+        sample_scale = _f32(sample_scale) if sample_scale is not None else None
         x = torch.empty(a.shape, device=a.device, dtype=torch.float32)
         xb = torch.empty(a.shape, device=a.device, dtype=torch.bfloat16)
         mean = torch.empty(rows, device=a.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=a.device, dtype=torch.float32)
-        call("hvk_ln_residual_fwd", ptr(a), ptr(x0), ptr(gamma), ptr(beta), ptr(sample_scale),
-             rows, C, rows_per_sample, float(eps), ptr(x), ptr(xb), ptr(mean), ptr(rstd),
-             stream())
-        ctx.save_for_backward(a, gamma, sample_scale, mean, rstd)
+        call("hvk_ln_residual_fwd", ptr(a), ptr(abias), ptr(x0), ptr(gamma), ptr(beta),
+             ptr(sample_scale), rows, C, rows_per_sample, float(eps), ptr(x), ptr(xb), ptr(mean),
+             ptr(rstd), stream())
+        ctx.save_for_backward(a, abias, gamma, sample_scale, mean, rstd)
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
         return x, xb
 
     @staticmethod
     def backward(ctx, gx, gxb):
-        a, gamma, sample_scale, mean, rstd = ctx.saved_tensors
+        a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
         C = a.shape[-1]
         rows = a.numel() // C
         gx = _f32(gx) if gx is not None else None
         gxb = _bf16(gxb) if gxb is not None else None
         if gx is None and gxb is None:
-            return (None,) * 7
+            return (None,) * 8
         ga = torch.empty_like(a)
         gx0 = torch.empty(a.shape, device=a.device, dtype=torch.float32) if ctx.has_x0 else None
         dgamma = torch.empty_like(gamma)
         dbeta = torch.empty_like(gamma)
+        dabias = torch.empty_like(gamma) if abias is not None else None
         ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
         ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
-        call("hvk_ln_residual_bwd", ptr(a), ptr(gamma), ptr(sample_scale), ptr(mean), ptr(rstd),
-             ptr(gx), ptr(gxb), rows, C, ctx.rps, ptr(gx0), ptr(ga), ptr(dgamma), ptr(dbeta),
-             ptr(ws), ws_bytes, stream())
-        return ga, gx0, dgamma, dbeta, None, None, None
+        call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
+             ptr(rstd), ptr(gx), ptr(gxb), rows, C, ctx.rps, ptr(gx0), ptr(ga), ptr(dgamma),
+             ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream())
+        return ga, dabias, gx0, dgamma, dbeta, None, None, None
 
 
-def layer_norm_residual(a, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5):
-    return LayerNormResidual.apply(a, x0, gamma, beta, sample_scale, rows_per_sample, eps)
+def layer_norm_residual(a, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5,
+                        abias=None):
+    return LayerNormResidual.apply(a, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps)
+
+
+# --------------------------------------------------------------------------- MLP activation
+class BiasGelu(torch.autograd.Function):
+    """y = GELU(h + b) (exact erf form); backward also returns db (column sums)."""
+
+    @staticmethod
+    def forward(ctx, h, bias):
+        h = _bf16(h)
+        N = h.shape[-1]
+        rows = h.numel() // N
+        bias = _f32(bias) if bias is not None else None
+        y = torch.empty_like(h)
+        call("hvk_bias_gelu_fwd", ptr(h), ptr(bias), ptr(y), rows, N, stream())
+        ctx.save_for_backward(h, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        h, bias = ctx.saved_tensors
+        N = h.shape[-1]
+        rows = h.numel() // N
+        gy = _bf16(gy)
+        gh = torch.empty_like(h)
+        db = torch.empty(N, device=h.device, dtype=torch.float32) if bias is not None else None
+        ws_bytes = _lib.load().hvk_bias_gelu_bwd_workspace_bytes(N)
+        ws = torch.empty(ws_bytes // 4, device=h.device, dtype=torch.float32)
+        call("hvk_bias_gelu_bwd", ptr(h), ptr(bias), ptr(gy), ptr(gh), ptr(db), ptr(ws), ws_bytes,
+             rows, N, stream())
+        return gh, db
+
+
+def bias_gelu(h, bias):
+    return BiasGelu.apply(h, bias)
 
 
 # --------------------------------------------------------------------------- PatchMerging

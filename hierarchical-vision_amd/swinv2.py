@@ -116,8 +116,13 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        h = self.drop(self.act(ops.linear(x, self.fc1.weight, self.fc1.bias)))
-        return self.drop(ops.linear(h, self.fc2.weight, self.fc2.bias))
+        return self.drop(ops.linear(self.hidden(x), self.fc2.weight, self.fc2.bias))
+
+    def hidden(self, x):
+        """GELU(fc1(x)) with the bias add fused into the activation kernel."""
+        if not isinstance(self.act, nn.GELU) or self.act.approximate != "none":
+            return self.drop(self.act(ops.linear(x, self.fc1.weight, self.fc1.bias)))
+        return self.drop(ops.bias_gelu(ops.linear(x, self.fc1.weight), self.fc1.bias))
 
 
 class WindowAttention(nn.Module):
@@ -176,12 +181,13 @@ class WindowAttention(nn.Module):
             return None
         return torch.cat((self.q_bias, torch.zeros_like(self.v_bias, requires_grad=False), self.v_bias))
 
-    def forward_tokens(self, x, H, W, shift):
-        """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] (after proj)."""
+    def forward_tokens(self, x, H, W, shift, proj_bias=True):
+        """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] after proj (without
+        proj's bias when proj_bias=False: the caller folds it into the next kernel)."""
         qkv = ops.linear(x, self.qkv.weight, self.qkv_bias_vector())
         o = ops.window_attention_core(qkv, self.bias_table(), self.scales(), H, W, self.num_heads,
                                       self.window_size[0], shift)
-        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj.bias))
+        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj.bias if proj_bias else None))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -250,14 +256,17 @@ class SwinTransformerBlock(nn.Module):
         H, W = self.input_resolution
         B, L, C = s.f32.shape
         assert L == H * W, "input feature has wrong size"
-        a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size)
+        fold = self.attn.proj_drop.p == 0 or not self.training  # proj bias -> LN kernel
+        a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold)
         dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
-                                        self.norm1.eps)
-        h = self.mlp(xb)
+                                        self.norm1.eps, abias=self.attn.proj.bias if fold else None)
+        fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
+        hid = self.mlp.hidden(xb)
+        h = self.mlp.drop(ops.linear(hid, self.mlp.fc2.weight, None if fold else self.mlp.fc2.bias))
         dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(h, x, self.norm2.weight, self.norm2.bias, dp, L,
-                                        self.norm2.eps)
+                                        self.norm2.eps, abias=self.mlp.fc2.bias if fold else None)
         return ResidualStream(x, xb)
 
     def forward(self, x):
@@ -382,11 +391,12 @@ class PatchEmbed(nn.Module):
         gh, gw = self.patches_resolution
         xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
         patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * ph * pw)
-        y = ops.linear(patches, self.proj.weight.reshape(self.embed_dim, -1), self.proj.bias)
+        w = self.proj.weight.reshape(self.embed_dim, -1)
         if self.norm is None:
-            return _as_stream(y)
+            return _as_stream(ops.linear(patches, w, self.proj.bias))
+        y = ops.linear(patches, w)
         x32, x16 = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1,
-                                           self.norm.eps)
+                                           self.norm.eps, abias=self.proj.bias)
         return ResidualStream(x32, x16)
 
     def forward(self, x):

@@ -51,27 +51,39 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bia
                  size_t workspace_bytes, int B, int H, int W, int C, int num_heads, int window,
                  int shift, void* stream);
 
-/* ---- Post-norm residual LayerNorm --------------------------------------------------
- * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a) (gamma, beta, eps)
- * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(x))), and with x0 == NULL the
- * plain norms of swinv2.py:494 (PatchMerging), 656 (patch_embed.norm), 833 (final norm).
- * a: bf16 [rows, C]; x0: f32 [rows, C] or NULL; sample_scale: f32 [rows/rows_per_sample]
- * or NULL (= 1; DropPath keep-mask / keep_prob); x_out: f32 [rows, C]; xb_out: bf16 copy
- * of x_out or NULL; mean/rstd: f32 [rows] saved for the backward. */
-int hvk_ln_residual_fwd(const void* a, const float* x0, const float* gamma, const float* beta,
-                        const float* sample_scale, int rows, int C, int rows_per_sample,
-                        float eps, float* x_out, void* xb_out, float* mean, float* rstd,
-                        void* stream);
+/* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
+ * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)
+ * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(proj(x))) with proj/fc2 run
+ * as GEMMs WITHOUT their bias), and with x0 == NULL the plain norms of swinv2.py:494
+ * (PatchMerging), 656 (patch_embed.norm), 833 (final norm).
+ * a: bf16 [rows, C]; abias: f32 [C] or NULL; x0: f32 [rows, C] or NULL; sample_scale:
+ * f32 [rows/rows_per_sample] or NULL (= 1; DropPath keep-mask / keep_prob); x_out:
+ * f32 [rows, C]; xb_out: bf16 copy of x_out or NULL; mean/rstd: f32 [rows] for the
+ * backward.  C: multiple of 8, <= 1024. */
+int hvk_ln_residual_fwd(const void* a, const float* abias, const float* x0, const float* gamma,
+                        const float* beta, const float* sample_scale, int rows, int C,
+                        int rows_per_sample, float eps, float* x_out, void* xb_out, float* mean,
+                        float* rstd, void* stream);
 /* gx: f32 [rows, C] or NULL, gxb: bf16 [rows, C] or NULL -- the two gradients of the
  * output (f32 residual stream and its bf16 copy), summed.  gx0: f32 [rows, C] or NULL
- * (gradient to the shortcut); ga: bf16 [rows, C]; dgamma/dbeta: f32 [C] (overwritten).
- * workspace: f32, hvk_ln_bwd_workspace_bytes(C) bytes. */
+ * (gradient to the shortcut); ga: bf16 [rows, C]; dgamma/dbeta/dabias: f32 [C]
+ * (overwritten; dabias = column sums of ga, may be NULL).  workspace: f32,
+ * hvk_ln_bwd_workspace_bytes(C) bytes. */
 size_t hvk_ln_bwd_workspace_bytes(int C);
-int hvk_ln_residual_bwd(const void* a, const float* gamma, const float* sample_scale,
-                        const float* mean, const float* rstd, const float* gx, const void* gxb,
-                        int rows, int C, int rows_per_sample, float* gx0, void* ga,
-                        float* dgamma, float* dbeta, float* workspace, size_t workspace_bytes,
-                        void* stream);
+int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
+                        const float* sample_scale, const float* mean, const float* rstd,
+                        const float* gx, const void* gxb, int rows, int C, int rows_per_sample,
+                        float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
+                        float* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- MLP activation: y = GELU(h + bias), exact erf form (swinv2.py:60-62, nn.GELU) ---
+ * h: bf16 [rows, N] = fc1 GEMM output without bias; bias: f32 [N] or NULL; y: bf16.
+ * Backward: gh = gy * GELU'(h + bias) (bf16) and dbias = column sums of gh (f32 [N],
+ * overwritten, may be NULL; needs hvk_bias_gelu_bwd_workspace_bytes(N) of workspace). */
+int hvk_bias_gelu_fwd(const void* h, const float* bias, void* y, int rows, int N, void* stream);
+size_t hvk_bias_gelu_bwd_workspace_bytes(int N);
+int hvk_bias_gelu_bwd(const void* h, const float* bias, const void* gy, void* gh, float* dbias,
+                      float* workspace, size_t workspace_bytes, int rows, int N, void* stream);
 
 /* ---- PatchMerging 2x2 gather (swinv2.py:484-491) -----------------------------------
  * out[b, (i, j), k*C + c] = x[b, (2i + dh_k, 2j + dw_k), c],

@@ -250,3 +250,53 @@ def test_hxe_with_non_identity_leaf_order():
     fn = HierarchicalCrossEntropy(tax, tree_weights="exponential").cuda()
     loss = fn(torch.from_numpy(z).cuda(), torch.from_numpy(tax.leaf_paths[leaves]).cuda())
     assert abs(loss.item() - ref) < 1e-4 * max(1.0, abs(ref))
+
+
+@pytest.mark.parametrize("C", [96, 768, 128])
+def test_layernorm_folded_bias_vs_torch(C):
+    import hvamd.ops as ops
+    B, L = 2, 37
+    a = torch.randn(B, L, C, device="cuda").bfloat16().requires_grad_(True)
+    ab = (0.3 * torch.randn(C, device="cuda")).requires_grad_(True)
+    gma = (1 + 0.1 * torch.randn(C, device="cuda")).requires_grad_(True)
+    bta = (0.1 * torch.randn(C, device="cuda")).requires_grad_(True)
+    x, xb = ops.layer_norm_residual(a, None, gma, bta, None, 1, 1e-5, abias=ab)
+    ref = torch.nn.functional.layer_norm(a.float() + ab, (C,), gma, bta, 1e-5)
+    assert rel(x.detach().cpu(), ref.detach().cpu()) < 1e-5
+    g = torch.randn_like(x)
+    x.backward(g)
+    mine = [t.grad.float().clone() for t in (a, ab, gma, bta)]
+    for t in (a, ab, gma, bta):
+        t.grad = None
+    ref.backward(g)
+    for m_, t in zip(mine, (a, ab, gma, bta)):
+        assert rel(m_.cpu(), t.grad.float().cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("N", [384, 3072, 96])
+def test_bias_gelu_vs_torch(N):
+    import hvamd.ops as ops
+    h = torch.randn(300, N, device="cuda").bfloat16().requires_grad_(True)
+    b = (0.5 * torch.randn(N, device="cuda")).requires_grad_(True)
+    y = ops.bias_gelu(h, b)
+    ref = torch.nn.functional.gelu(h.float() + b)
+    assert rel(y.float().detach().cpu(), ref.detach().cpu()) < 5e-3
+    g = torch.randn_like(ref)
+    y.backward(g.bfloat16())
+    mh, mb = h.grad.float().clone(), b.grad.clone()
+    h.grad = None
+    b.grad = None
+    ref.backward(g)
+    assert rel(mh.cpu(), h.grad.float().cpu()) < 1e-2
+    assert rel(mb.cpu(), b.grad.cpu()) < 1e-2
+
+
+def test_mlp_vs_reference(golden):
+    from hvamd.swinv2 import Mlp
+    g = golden("module_golden")
+    m = _load(Mlp(in_features=32, hidden_features=128), 60)
+    y, x = _run(m, "mlp.", g)
+    assert rel(y.detach().float().cpu(), g["mlp.y"]) < 1e-2
+    assert rel(x.grad.float().cpu(), g["mlp.gx"]) < 2e-2
+    for k, p in m.named_parameters():
+        assert rel(p.grad.float().cpu(), g["mlp.grad." + k]) < 2e-2, k
