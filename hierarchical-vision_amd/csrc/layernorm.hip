@@ -225,8 +225,8 @@ __global__ __launch_bounds__(64) void colsum_kernel(const float* part, int nblk,
     for (int u = 0; u < 8; ++u) s[u] += part[(size_t)(b + u * kRedRowGroups) * ncol + c];
   for (; b < nblk; b += kRedRowGroups) s[0] += part[(size_t)b * ncol + c];
   const float v = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  float* dst = c < C ? out0 + c : (c < 2 * C ? out1 + (c - C) : out2 + (c - 2 * C));
-  if (dst) atomicAdd(dst, v);
+  float* base = c < C ? out0 : (c < 2 * C ? out1 : out2);
+  if (base) atomicAdd(base + (c % C), v);  // NULL output (e.g. no folded bias): skip
 }
 
 constexpr int kBwdBlocks = 1024;
