@@ -61,6 +61,10 @@ def build(args, device):
         info = models.DatasetInfo(num_classes=tax.num_classes, taxonomy=tax)
     else:
         info = models.DatasetInfo(num_classes=1000)
+    # reference optimizer (DecoupledSGDW, momentum 0.875, wd 5e-4; configs.py:421-425) at an
+    # lr that does not diverge from random init (2.048 is tuned for ResNet-50 at batch 2048);
+    # the work per step does not depend on it
+    cfg.optim.lr = 0.02
     model = models.build_composer_model(cfg, info).to(device)
     opt = optim.build_optimizer(cfg, model)
     trainer = Trainer(model, opt, [GradientClipping("norm", 2.0)])
