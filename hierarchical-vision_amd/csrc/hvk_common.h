@@ -39,8 +39,11 @@ __device__ __forceinline__ float hvk_hi(uint32_t w) { return __uint_as_float(w &
 __device__ __forceinline__ uint32_t hvk_f2bf(float f) {
   return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)f);  // RNE, v_cvt_pk_bf16_f32
 }
+typedef float hvk_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 hvk_bf16x2 __attribute__((ext_vector_type(2)));
+// two f32 -> packed bf16x2 (RNE) in ONE v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t hvk_pack2(float lo, float hi) {
-  return hvk_f2bf(lo) | (hvk_f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((hvk_f32x2){lo, hi}, hvk_bf16x2));
 }
 __device__ __forceinline__ void hvk_unpack8(const uint4& v, float f[8]) {
   f[0] = hvk_lo(v.x); f[1] = hvk_hi(v.x); f[2] = hvk_lo(v.y); f[3] = hvk_hi(v.y);
@@ -65,6 +68,29 @@ __device__ __forceinline__ uint2 hvk_tr_read(const hvk_bf16* lds) {
   hvk_i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(HVK_LDS_I16X4(lds));
   return __builtin_bit_cast(uint2, r);
 }
+
+// Reductions over the 4 lanes l, l^16, l^32, l^48 (the 4 k-groups of a 16x16x32 MFMA
+// fragment) with v_permlane16_swap / v_permlane32_swap: VALU only, no LDS round trip.
+// With both operands = v, the two swap results hold v[l] and v[l ^ 16] (or ^ 32) in some
+// order, so their sum / max is the pairwise reduction in every lane.
+__device__ __forceinline__ float hvk_xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float hvk_xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float hvk_xor16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float hvk_xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float hvk_group4_sum(float v) { return hvk_xor32_sum(hvk_xor16_sum(v)); }
+__device__ __forceinline__ float hvk_group4_max(float v) { return hvk_xor32_max(hvk_xor16_max(v)); }
 
 __device__ __forceinline__ float hvk_wave_sum(float v) {
 #pragma unroll

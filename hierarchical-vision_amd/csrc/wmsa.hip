@@ -18,12 +18,14 @@
 // Layout per (window, head) pair, one wave each: N = WIN^2 tokens padded to
 // NT = ceil(N/16) tiles of 16; head_dim = 32 = one K-step of
 // v_mfma_f32_16x16x32_bf16.  S^T = K Q^T keeps one query per lane column so
-// the softmax row reduction is in-lane (16 values) + 2 xor-shuffles; the S^T
+// the softmax row reduction is in-lane (16 values) + 2 permlane swaps; the S^T
 // accumulators feed P*V directly as the MFMA B operand (k-order permuted
 // consistently, see hvk_common.h); V^T comes from LDS through
 // ds_read_b64_tr_b16.  Bias (rpi gather of the CPB table) is expanded once per
 // workgroup into an LDS table laid out in accumulator order; the shift mask is
 // recomputed from region bits only on edge windows.
+#include <stdlib.h>
+
 #include "hvk_common.h"
 
 namespace {
@@ -34,8 +36,14 @@ constexpr int kThreads = 64 * kWaves;
 struct WmsaGeom {
   int B, H, W, C, nH, shift;
   int nWh, nWw, n_windows;   // windows per image row/col, total windows (B*nWh*nWw)
-  int n_chunks, wpc;         // per head: chunks (un-padded) and windows per chunk
+  int n_chunks;              // window chunks per head (multiple of 8: XCD groups)
 };
+
+// balanced split of the windows over the chunks of one head
+__device__ __forceinline__ void chunk_range(const WmsaGeom& g, int chunk, int& w0, int& w1) {
+  w0 = (int)((long long)chunk * g.n_windows / g.n_chunks);
+  w1 = (int)((long long)(chunk + 1) * g.n_windows / g.n_chunks);
+}
 
 template <int WIN>
 struct WinCfg {
@@ -53,7 +61,10 @@ struct WinCfg {
 template <int WIN>
 __device__ void build_bias_table(float* tab, const float* __restrict__ src) {
   using K = WinCfg<WIN>;
-  for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
+  static_assert(K::TAB % kThreads == 0, "table is a whole number of block strides");
+#pragma unroll  // all loads of the (L2-resident) source table in flight together
+  for (int k = 0; k < K::TAB / kThreads; ++k) {
+    const int e = threadIdx.x + k * kThreads;
     const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
     const int qi = blk / K::NT, ki = blk % K::NT;
     const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
@@ -81,17 +92,18 @@ __device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh
 }
 
 // L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
-__device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm) {
+__device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post = 1.f) {
   float f[8];
   hvk_unpack8(v, f);
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-  ss += __shfl_xor(ss, 16);
-  ss += __shfl_xor(ss, 32);
-  rnorm = 1.f / fmaxf(sqrtf(ss), 1e-12f);  // F.normalize: x / max(||x||, eps)
+  ss = hvk_group4_sum(ss);
+  // F.normalize: x / max(||x||, eps) == x * rsqrt(max(||x||^2, eps^2))
+  rnorm = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
+  const float m = rnorm * post;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] *= rnorm;
+  for (int j = 0; j < 8; ++j) f[j] *= m;
   return hvk_pack8(f);
 }
 
@@ -134,7 +146,8 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
   int chunk, h;
   hvk_decode_chunk_head(blockIdx.x, g.nH, chunk, h);
   if (chunk >= g.n_chunks) return;
-  const int w0 = chunk * g.wpc, w1 = min(w0 + g.wpc, g.n_windows);
+  int w0, w1;
+  chunk_range(g, chunk, w0, w1);
   if (w0 >= w1) return;
 
   float* btab = reinterpret_cast<float*>(smem);
@@ -161,26 +174,50 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       const int t = 16 * i + li;
       row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
       if (t < K::N) {
+#ifdef HVK_PROBE_CONTIGUOUS  // tools/probe: same byte count, fully contiguous 1-KB wave reads
+        const size_t nblk = (size_t)g.B * g.H * g.W * 3 * C / 1536;
+        const size_t blk = ((size_t)(w * g.nH + h) * K::NT + i) % nblk;
+        const hvk_bf16* p = a.qkv + blk * 1536 + 8 * lane;
+        qf[i] = *reinterpret_cast<const uint4*>(p);
+        kf[i] = *reinterpret_cast<const uint4*>(p + 512);
+        vf[i] = *reinterpret_cast<const uint4*>(p + 1024);
+#else
         const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
         qf[i] = *reinterpret_cast<const uint4*>(p);
         kf[i] = *reinterpret_cast<const uint4*>(p + C);
         vf[i] = *reinterpret_cast<const uint4*>(p + 2 * C);
+#endif
       } else {
         qf[i] = kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
       }
     }
+#ifdef HVK_PROBE_MEMORY_ONLY  // tools/probe: same gather/scatter, no math (memory ceiling)
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i)
+      if (16 * i + li < K::N) {
+        uint4 t = qf[i];
+        t.x ^= kf[i].x ^ vf[i].x; t.y ^= kf[i].y ^ vf[i].y;
+        t.z ^= kf[i].z ^ vf[i].z; t.w ^= kf[i].w ^ vf[i].w;
+#ifdef HVK_PROBE_CONTIGUOUS_STORE
+        const size_t nb = (size_t)g.B * g.H * g.W * C / 512;
+        *reinterpret_cast<uint4*>(a.out + (((size_t)(w * g.nH + h) * K::NT + i) % nb) * 512 + 8 * lane) = t;
+#else
+        *reinterpret_cast<uint4*>(a.out + (size_t)row[i] * C + h * 32 + 8 * gq) = t;
+#endif
+      }
+    continue;
+#endif
     float rn;
 #pragma unroll
     for (int i = 0; i < K::NT; ++i) {
-      qf[i] = l2_normalize(qf[i], rn);
+      qf[i] = l2_normalize(qf[i], rn, sc2);  // q^ * scale * log2e: the MFMA applies the scale
       kf[i] = l2_normalize(kf[i], rn);
       *reinterpret_cast<uint4*>(vst + (16 * i + li) * 32 + 8 * gq) = vf[i];
     }
 #pragma unroll
     for (int i = K::NT; i < 2 * K::NC; ++i)
       *reinterpret_cast<uint4*>(vst + (16 * i + li) * 32 + 8 * gq) = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
     // V^T fragments (A operand of O^T = V^T P^T), key order per chunk c, lane group g, slot j:
     // key(g, j) = 32c + (j < 4 ? 4g + j : 16 + 4g + j - 4)
     uint4 vt[K::NC][2];
@@ -198,18 +235,14 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       // keep one query tile live at a time and the bias-table reads inside the loop (VGPR budget)
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+      // S'^T = K^ (scale log2e Q^)^T + bias: the bias tile rides in as the MFMA C operand
       hvk_f32x4 s[K::NT];
-#pragma unroll
-      for (int ki = 0; ki < K::NT; ++ki) s[ki] = hvk_mfma16(kf[ki], qf[qi], hvk_f32x4{0, 0, 0, 0});
-      const int q = 16 * qi + li;
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki) {
         const float4 bb = *reinterpret_cast<const float4*>(btab + ((qi * K::NT + ki) * 64 + lane) * 4);
-        s[ki][0] = s[ki][0] * sc2 + bb.x;
-        s[ki][1] = s[ki][1] * sc2 + bb.y;
-        s[ki][2] = s[ki][2] * sc2 + bb.z;
-        s[ki][3] = s[ki][3] * sc2 + bb.w;
+        s[ki] = hvk_mfma16(kf[ki], qf[qi], hvk_f32x4{bb.x, bb.y, bb.z, bb.w});
       }
+      const int q = 16 * qi + li;
       if (edge_r || edge_c) {  // wave-uniform: only the last window row / column carries a mask
         const uint32_t mm = mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c);
 #pragma unroll
@@ -222,19 +255,17 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       for (int ki = 0; ki < K::NT; ++ki)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[ki][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = hvk_group4_max(mx);
       float sum = 0.f;
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[ki][r] - mx);
+          const float p = __builtin_amdgcn_exp2f(s[ki][r] - mx);
           s[ki][r] = p;
           sum += p;
         }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
+      sum = hvk_group4_sum(sum);
       hvk_f32x4 o[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
       for (int c = 0; c < K::NC; ++c) {
@@ -246,7 +277,7 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
         o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
       }
       if (q < K::N) {
-        const float inv = 1.f / sum;
+        const float inv = __builtin_amdgcn_rcpf(sum);
         hvk_bf16* dst = a.out + (size_t)row[qi] * C + h * 32 + 4 * gq;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
@@ -284,7 +315,8 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
   int chunk, h;
   hvk_decode_chunk_head(blockIdx.x, g.nH, chunk, h);
   if (chunk >= g.n_chunks) return;
-  const int w0 = chunk * g.wpc, w1 = min(w0 + g.wpc, g.n_windows);
+  int w0, w1;
+  chunk_range(g, chunk, w0, w1);
   if (w0 >= w1) return;
 
   float* btab = reinterpret_cast<float*>(smem);
@@ -343,8 +375,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       *reinterpret_cast<uint4*>(ks + (16 * i + li) * 32 + 8 * gq) = kf[i];
       *reinterpret_cast<uint4*>(dos + (16 * i + li) * 32 + 8 * gq) = df[i];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
     // K^T fragments for dQ^T = K^T dS^T (k = key, permuted order as in the forward)
     uint4 kt_frag[K::NC][2];
 #pragma unroll
@@ -389,19 +420,17 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       for (int ki = 0; ki < K::NT; ++ki)
 #pragma unroll
         for (int r = 0; r < 4; ++r) mx = fmaxf(mx, p[ki][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      mx = hvk_group4_max(mx);
       float sum = 0.f;
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[ki][r] = exp2f(p[ki][r] - mx);
+          p[ki][r] = __builtin_amdgcn_exp2f(p[ki][r] - mx);
           sum += p[ki][r];
         }
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
-      const float inv = 1.f / sum;
+      sum = hvk_group4_sum(sum);
+      const float inv = __builtin_amdgcn_rcpf(sum);
       float delta = 0.f;
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki)
@@ -410,8 +439,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
           p[ki][r] *= inv;
           delta += p[ki][r] * dp[ki][r];
         }
-      delta += __shfl_xor(delta, 16);
-      delta += __shfl_xor(delta, 32);
+      delta = hvk_group4_sum(delta);
       float ds[K::NT][4];
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki) {
@@ -452,8 +480,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) dot += qh[dt][r] * dq[dt][r];
       }
-      dot += __shfl_xor(dot, 16);
-      dot += __shfl_xor(dot, 32);
+      dot = hvk_group4_sum(dot);
       if (rnq[qi] >= 1e12f) dot = 0.f;  // ||q|| <= eps: x / eps, no projection term
       if (q < K::N) {
         hvk_bf16* dst = a.dqkv + (size_t)row[qi] * C3 + h * 32 + 4 * gq;
@@ -467,8 +494,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
 
     // ---------------- phase B: one key tile at a time, key on the lane
     // query chunk c, slot (g, j): q(g, j) = 32c + (j < 4 ? 4g + j : 16 + 4g + j - 4)
@@ -504,8 +530,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) dot += kh[dt][r] * dk[dt][r];
       }
-      dot += __shfl_xor(dot, 16);
-      dot += __shfl_xor(dot, 32);
+      dot = hvk_group4_sum(dot);
       if (rnk[kt] >= 1e12f) dot = 0.f;
       if (key < K::N) {
         hvk_bf16* dst = a.dqkv + (size_t)row[kt] * C3 + h * 32 + 4 * gq;
@@ -521,8 +546,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
         }
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
   }
 
   // ---- workgroup reduction of the bias / scale gradients, then one atomic per entry
@@ -580,7 +604,9 @@ constexpr size_t bwd_lds_bytes() {
   return WinCfg<WIN>::TAB * 4 + kWaves * (size_t)(ROWS * 32 * 3 + ROWS * ROWS * 2) * 2;
 }
 
-int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int target_wgs, WmsaGeom& g) {
+// Persistent grid: n_heads * n_chunks <= `capacity` resident workgroups (no tail round),
+// n_chunks a multiple of 8 so every XCD group holds whole (chunk, all heads) sets.
+int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int capacity, WmsaGeom& g) {
   if (B <= 0 || H <= 0 || W <= 0 || nH <= 0)
     return hvk_set_error(HVK_EINVAL, "wmsa: bad shape B=%d H=%d W=%d nH=%d", B, H, W, nH);
   if (C != 32 * nH)
@@ -592,16 +618,16 @@ int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int target
   g.B = B; g.H = H; g.W = W; g.C = C; g.nH = nH; g.shift = shift;
   g.nWh = H / win; g.nWw = W / win;
   g.n_windows = B * g.nWh * g.nWw;
-  int chunks = (target_wgs + nH - 1) / nH;
-  chunks = chunks < 1 ? 1 : chunks;
-  g.wpc = (g.n_windows + chunks - 1) / chunks;
-  g.n_chunks = (g.n_windows + g.wpc - 1) / g.wpc;
+  int chunks = capacity / nH / 8 * 8;
+  if (chunks < 8) chunks = 8;
+  const int need = (g.n_windows + 7) / 8 * 8;  // never more chunks than windows (rounded)
+  g.n_chunks = chunks < need ? chunks : need;
   return HVK_OK;
 }
 
 template <int WIN>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
-  const int padded = (a.g.n_chunks + 7) / 8 * 8;
+  const int padded = a.g.n_chunks;  // already a multiple of 8
   const size_t lds = fwd_lds_bytes<WIN>();
   hipLaunchKernelGGL(wmsa_fwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd");
@@ -610,7 +636,7 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 
 template <int WIN>
 int launch_bwd(const BwdArgs& a, float* dbias_table, hipStream_t st) {
-  const int padded = (a.g.n_chunks + 7) / 8 * 8;
+  const int padded = a.g.n_chunks;  // already a multiple of 8
   const size_t lds = bwd_lds_bytes<WIN>();
   static bool attr_set = false;
   if (!attr_set) {
@@ -644,10 +670,13 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
   a.out = static_cast<hvk_bf16*>(out);
   a.bias = bias_table;
   a.scale = scale;
-  // ~16 windows per workgroup (4 per wave)
-  const int nwin = B * (H / (window > 0 ? window : 1)) * (W / (window > 0 ? window : 1));
-  const int target = ((nwin + 15) / 16) * num_heads;
-  int rc = make_geom(B, H, W, C, num_heads, window, shift, target, a.g);
+  // resident workgroups: 256 CUs x 4 (<=128 VGPRs -> 4 waves/SIMD); HVK_WMSA_FWD_WGS overrides
+  static const int cap = [] {
+    const char* e = getenv("HVK_WMSA_FWD_WGS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 256 * 4;
+  }();
+  int rc = make_geom(B, H, W, C, num_heads, window, shift, cap, a.g);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (window) {
@@ -676,8 +705,8 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bia
   a.scale = scale;
   a.dbias_acc = workspace;
   a.dscale = dscale;
-  // one resident 4-wave workgroup per CU (LDS-bound), two rounds over the chip
-  int rc = make_geom(B, H, W, C, num_heads, window, shift, 512, a.g);
+  // one resident 4-wave workgroup per CU (128 KB LDS, 1 wave/SIMD)
+  int rc = make_geom(B, H, W, C, num_heads, window, shift, 256, a.g);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hipMemsetAsync(workspace, 0, hvk_wmsa_bwd_workspace_bytes(num_heads, window), st) != hipSuccess ||

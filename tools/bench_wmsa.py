@@ -1,0 +1,84 @@
+"""Microbenchmark of the W-MSA kernels on the SwinV2-T bs256 stage shapes.
+
+    python tools/bench_wmsa.py [--iters 20]
+
+Prints, per stage, forward and backward time per launch and algorithmic GB/s
+(8*T*C forward, 16*T*C backward), on random bf16 inputs."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+STAGES = [  # (name, B, H, W, C, heads, window, shift, blocks per step)
+    ("stage0-s3", 256, 56, 56, 96, 3, 7, 3, 2),
+    ("stage1-s3", 256, 28, 28, 192, 6, 7, 3, 2),
+    ("stage2-s3", 256, 14, 14, 384, 12, 7, 3, 6),
+    ("stage3", 256, 7, 7, 768, 24, 7, 0, 2),
+]
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="alternative libhvk build (tools/probe)")
+    args = ap.parse_args()
+    from hvamd import _lib
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
+    lib = _lib.load()
+    tot_f = tot_b = 0.0
+    byt_f = byt_b = 0
+    for name, B, H, W, C, nh, win, sh, nblk in STAGES:
+        T = B * H * W
+        qkv = torch.randn(T, 3 * C, device="cuda").bfloat16()
+        out = torch.empty(T, C, device="cuda", dtype=torch.bfloat16)
+        dout = torch.randn(T, C, device="cuda").bfloat16()
+        dqkv = torch.empty_like(qkv)
+        tab = 16 * torch.sigmoid(torch.randn(nh, (2 * win - 1) ** 2, device="cuda"))
+        scale = torch.full((nh,), 10.0, device="cuda")
+        dtab = torch.empty_like(tab)
+        dsc = torch.empty_like(scale)
+        wsb = lib.hvk_wmsa_bwd_workspace_bytes(nh, win)
+        ws = torch.empty(wsb // 4, device="cuda")
+        P = _lib.ptr
+        st = _lib.stream
+
+        def fwd():
+            _lib.call("hvk_wmsa_fwd", P(qkv), P(out), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
+
+        def bwd():
+            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(dqkv), P(tab), P(scale), P(dtab), P(dsc),
+                      P(ws), wsb, B, H, W, C, nh, win, sh, st())
+
+        tf = timeit(fwd, args.iters)
+        tb = timeit(bwd, args.iters)
+        bf, bb = 8 * T * C, 16 * T * C
+        tot_f += tf * nblk
+        tot_b += tb * nblk
+        byt_f += bf * nblk
+        byt_b += bb * nblk
+        print(f"{name:10s} fwd {tf * 1e3:8.1f} us {bf / tf / 1e6:7.0f} GB/s | "
+              f"bwd {tb * 1e3:8.1f} us {bb / tb / 1e6:7.0f} GB/s", flush=True)
+        del qkv, out, dout, dqkv
+    print(f"per step: fwd {tot_f:.3f} ms ({byt_f / tot_f / 1e6:.0f} GB/s)  "
+          f"bwd {tot_b:.3f} ms ({byt_b / tot_b / 1e6:.0f} GB/s)")
+
+
+if __name__ == "__main__":
+    main()
