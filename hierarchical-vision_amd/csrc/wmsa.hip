@@ -130,6 +130,26 @@ __device__ __forceinline__ uint32_t mask_bits(uint32_t krow, uint32_t kcol, int 
   return (edge_r ? (krow ^ qr) : 0u) | (edge_c ? (kcol ^ qc) : 0u);
 }
 
+// The forward's LDS image of V keeps head_dim columns in the order
+// col 16dt + 4g + r <-> d = 8g + 4dt + r, so an MFMA that reads them as A = X^T through
+// ds_read_b64_tr_b16 puts d = 8g..8g+7 of one token in lane (g, token) across its two
+// accumulators (dt = 0, 1): every output row segment leaves as ONE 16-B store.  The lane
+// holding d = 8g..8g+7 of a token writes the two halves to cols 4g and 16 + 4g.
+// The 8-B column blocks (col8 = col/4) of a 64-B row are XOR-swizzled by (row>>1)&7: the
+// 16 rows of one write group then hit 32 distinct banks, and the tr-reads' row quads too.
+__device__ __forceinline__ int lds_off(int row, int col8) {
+  return row * 32 + ((col8 ^ ((row >> 1) & 7)) << 2);
+}
+__device__ __forceinline__ void lds_write_dperm(hvk_bf16* img, int row, int g, uint4 v) {
+  *reinterpret_cast<uint2*>(img + lds_off(row, g)) = make_uint2(v.x, v.y);
+  *reinterpret_cast<uint2*>(img + lds_off(row, 4 + g)) = make_uint2(v.z, v.w);
+}
+// the two accumulator quads of a lane (d = 8g + 4dt + r) as 8 packed bf16
+__device__ __forceinline__ uint4 pack_dperm(const float a[4], const float b[4]) {
+  return make_uint4(hvk_pack2(a[0], a[1]), hvk_pack2(a[2], a[3]), hvk_pack2(b[0], b[1]),
+                    hvk_pack2(b[2], b[3]));
+}
+
 struct FwdArgs {
   const hvk_bf16* qkv;       // [T, 3C]
   hvk_bf16* out;             // [T, C]
@@ -183,9 +203,9 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
         vf[i] = *reinterpret_cast<const uint4*>(p + 1024);
 #else
         const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
-        qf[i] = *reinterpret_cast<const uint4*>(p);
-        kf[i] = *reinterpret_cast<const uint4*>(p + C);
-        vf[i] = *reinterpret_cast<const uint4*>(p + 2 * C);
+        qf[i] = hvk_ld16(p);
+        kf[i] = hvk_ld16(p + C);
+        vf[i] = hvk_ld16(p + 2 * C);
 #endif
       } else {
         qf[i] = kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
@@ -212,7 +232,7 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
     for (int i = 0; i < K::NT; ++i) {
       qf[i] = l2_normalize(qf[i], rn, sc2);  // q^ * scale * log2e: the MFMA applies the scale
       kf[i] = l2_normalize(kf[i], rn);
-      *reinterpret_cast<uint4*>(vst + (16 * i + li) * 32 + 8 * gq) = vf[i];
+      lds_write_dperm(vst, 16 * i + li, gq, vf[i]);
     }
 #pragma unroll
     for (int i = K::NT; i < 2 * K::NC; ++i)
@@ -225,8 +245,8 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
     for (int c = 0; c < K::NC; ++c)
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const hvk_bf16* base = vst + (32 * c + 4 * gq + (li >> 2)) * 32 + 16 * dt + 4 * (li & 3);
-        const uint2 lo = hvk_tr_read(base), hi = hvk_tr_read(base + 16 * 32);
+        const int rr = 32 * c + 4 * gq + (li >> 2), c8 = 4 * dt + (li & 3);
+        const uint2 lo = hvk_tr_read(vst + lds_off(rr, c8)), hi = hvk_tr_read(vst + lds_off(rr + 16, c8));
         vt[c][dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
 
@@ -278,12 +298,9 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       }
       if (q < K::N) {
         const float inv = __builtin_amdgcn_rcpf(sum);
-        hvk_bf16* dst = a.out + (size_t)row[qi] * C + h * 32 + 4 * gq;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          *reinterpret_cast<uint2*>(dst + 16 * dt) =
-              make_uint2(hvk_pack2(o[dt][0] * inv, o[dt][1] * inv),
-                         hvk_pack2(o[dt][2] * inv, o[dt][3] * inv));
+        const float o0[4] = {o[0][0] * inv, o[0][1] * inv, o[0][2] * inv, o[0][3] * inv};
+        const float o1[4] = {o[1][0] * inv, o[1][1] * inv, o[1][2] * inv, o[1][3] * inv};
+        hvk_st16(a.out + (size_t)row[qi] * C + h * 32 + 8 * gq, pack_dperm(o0, o1));
       }
     }
   }
@@ -359,10 +376,10 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
       if (t < K::N) {
         const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
-        qf[i] = *reinterpret_cast<const uint4*>(p);
-        kf[i] = *reinterpret_cast<const uint4*>(p + C);
-        vf[i] = *reinterpret_cast<const uint4*>(p + 2 * C);
-        df[i] = *reinterpret_cast<const uint4*>(a.dout + (size_t)row[i] * C + h * 32 + 8 * gq);
+        qf[i] = hvk_ld16(p);
+        kf[i] = hvk_ld16(p + C);
+        vf[i] = hvk_ld16(p + 2 * C);
+        df[i] = hvk_ld16(a.dout + (size_t)row[i] * C + h * 32 + 8 * gq);
       } else {
         qf[i] = kf[i] = vf[i] = df[i] = make_uint4(0, 0, 0, 0);
       }
@@ -489,8 +506,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[qi];
-          *reinterpret_cast<uint2*>(dst + 16 * dt) =
-              make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+          hvk_st8(dst + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
         }
       }
     }
@@ -539,10 +555,9 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rnk[kt];
-          *reinterpret_cast<uint2*>(dst + C + 16 * dt) =
-              make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
-          *reinterpret_cast<uint2*>(dst + 2 * C + 16 * dt) =
-              make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
+          hvk_st8(dst + C + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
+          hvk_st8(dst + 2 * C + 16 * dt,
+                  make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
         }
       }
     }
