@@ -20,10 +20,12 @@ _sz = ctypes.c_size_t
 # name -> (restype, argtypes); kept in the order of include/hvk.h
 SIGNATURES = {
     "hvk_abi_version": (_i, []),
+    "hvk_kernel_timer_enable": (_i, [_i]),
+    "hvk_kernel_timer_read": (_i, [_i, _p, _p]),
     "hvk_last_error_string": (ctypes.c_char_p, []),
     "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
-    "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),
     "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,

@@ -2,6 +2,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <vector>
+
 #include "hvk_common.h"
 
 static thread_local char g_hvk_err[512] = "";
@@ -18,6 +20,58 @@ int hvk_set_error(int code, const char* fmt, ...) {
 
 const char* hvk_last_error_string(void) { return g_hvk_err; }
 
-int hvk_abi_version(void) { return 1; }
+int hvk_abi_version(void) { return 2; }
+
+// ---- kernel timer ------------------------------------------------------------------
+namespace {
+struct TimerRec {
+  int kind;
+  hipEvent_t start, stop;
+};
+std::vector<TimerRec> g_timer;  // event pool (created once, reused)
+size_t g_timer_used = 0;
+bool g_timer_on = false;
+}  // namespace
+
+void hvk_timer_next(int kind, hipEvent_t* start, hipEvent_t* stop) {
+  if (!g_timer_on || g_timer_used >= g_timer.size()) {
+    *start = *stop = nullptr;
+    return;
+  }
+  TimerRec& r = g_timer[g_timer_used++];
+  r.kind = kind;
+  *start = r.start;
+  *stop = r.stop;
+}
+
+int hvk_kernel_timer_enable(int max_launches) {
+  g_timer_used = 0;
+  g_timer_on = max_launches > 0;
+  while (g_timer.size() < (size_t)(max_launches > 0 ? max_launches : 0)) {
+    TimerRec r{-1, nullptr, nullptr};
+    if (hipEventCreate(&r.start) != hipSuccess || hipEventCreate(&r.stop) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_enable: hipEventCreate failed");
+    g_timer.push_back(r);
+  }
+  return HVK_OK;
+}
+
+int hvk_kernel_timer_read(int kind, double* total_ms, int* launches) {
+  if (!total_ms || !launches) return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_read: null pointer");
+  double t = 0.0;
+  int n = 0;
+  for (size_t i = 0; i < g_timer_used; ++i) {
+    const TimerRec& r = g_timer[i];
+    if (r.kind != kind) continue;
+    float ms = 0.f;
+    if (hipEventSynchronize(r.stop) != hipSuccess || hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_read: event query failed");
+    t += ms;
+    ++n;
+  }
+  *total_ms = t;
+  *launches = n;
+  return HVK_OK;
+}
 
 }  // extern "C"

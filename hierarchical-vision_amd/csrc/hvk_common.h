@@ -1,6 +1,7 @@
 // Shared device helpers for libhvk (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -25,6 +26,28 @@ int hvk_set_error(int code, const char* fmt, ...);
 #define HVK_EINVAL 1
 #define HVK_EUNSUPPORTED 2
 #define HVK_EHIP 3
+
+// ---- opt-in kernel timer (capi.hip): start/stop events recorded by the dispatch packet
+// itself (hipExtLaunchKernelGGL), so a duration is the kernel's execution only, like a
+// rocprofv3 kernel trace (HIP events around a launch also count the dispatch gap).
+#define HVK_TIMER_WMSA_FWD 0
+#define HVK_TIMER_WMSA_BWD 1
+#ifdef __cplusplus
+extern "C" {
+#endif
+void hvk_timer_next(int kind, hipEvent_t* start, hipEvent_t* stop);  // null pair: not timed
+#ifdef __cplusplus
+}
+#endif
+#define HVK_LAUNCH_TIMED(kind, kernel, grid, block, lds, st, ...)                       \
+  do {                                                                                  \
+    hipEvent_t e0_ = nullptr, e1_ = nullptr;                                            \
+    hvk_timer_next(kind, &e0_, &e1_);                                                   \
+    if (e0_)                                                                            \
+      hipExtLaunchKernelGGL(kernel, grid, block, lds, st, e0_, e1_, 0, __VA_ARGS__);     \
+    else                                                                                \
+      hipLaunchKernelGGL(kernel, grid, block, lds, st, __VA_ARGS__);                    \
+  } while (0)
 
 #define HVK_CHECK_LAUNCH(what)                                                   \
   do {                                                                           \

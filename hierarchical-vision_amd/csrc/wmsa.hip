@@ -26,18 +26,14 @@
 // recomputed from region bits only on edge windows.
 #include <stdlib.h>
 
-#include "hvk_common.h"
+#include "wmsa_common.h"
 
 namespace {
+using namespace hvk_wmsa;
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 
-struct WmsaGeom {
-  int B, H, W, C, nH, shift;
-  int nWh, nWw, n_windows;   // windows per image row/col, total windows (B*nWh*nWw)
-  int n_chunks;              // window chunks per head (multiple of 8: XCD groups)
-};
 
 // balanced split of the windows over the chunks of one head
 __device__ __forceinline__ void chunk_range(const WmsaGeom& g, int chunk, int& w0, int& w1) {
@@ -81,31 +77,7 @@ __device__ void build_bias_table(float* tab, const float* __restrict__ src) {
   }
 }
 
-// token row (in the un-shifted [B*H*W] token order) of window position t
-__device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh, int ww, int win,
-                                                int t) {
-  int y = wh * win + t / win + g.shift;
-  int x = ww * win + t % win + g.shift;
-  if (y >= g.H) y -= g.H;
-  if (x >= g.W) x -= g.W;
-  return (b * g.H + y) * g.W + x;
-}
 
-// L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
-__device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post = 1.f) {
-  float f[8];
-  hvk_unpack8(v, f);
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-  ss = hvk_group4_sum(ss);
-  // F.normalize: x / max(||x||, eps) == x * rsqrt(max(||x||^2, eps^2))
-  rnorm = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
-  const float m = rnorm * post;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] *= m;
-  return hvk_pack8(f);
-}
 
 // Region bit of a window-local coordinate in the last window row/col (swinv2.py:359-375).
 template <int WIN>
@@ -150,13 +122,6 @@ __device__ __forceinline__ uint4 pack_dperm(const float a[4], const float b[4]) 
                     hvk_pack2(b[2], b[3]));
 }
 
-struct FwdArgs {
-  const hvk_bf16* qkv;       // [T, 3C]
-  hvk_bf16* out;             // [T, C]
-  const float* bias;         // [nH, R*R]   16*sigmoid(cpb)
-  const float* scale;        // [nH]        exp(clamp(logit_scale))
-  WmsaGeom g;
-};
 
 template <int WIN>
 __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
@@ -227,12 +192,13 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       }
     continue;
 #endif
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) lds_write_dperm(vst, 16 * i + li, gq, vf[i]);  // frees vf first
     float rn;
 #pragma unroll
     for (int i = 0; i < K::NT; ++i) {
       qf[i] = l2_normalize(qf[i], rn, sc2);  // q^ * scale * log2e: the MFMA applies the scale
       kf[i] = l2_normalize(kf[i], rn);
-      lds_write_dperm(vst, 16 * i + li, gq, vf[i]);
     }
 #pragma unroll
     for (int i = K::NT; i < 2 * K::NC; ++i)
@@ -306,16 +272,6 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
   }
 }
 
-struct BwdArgs {
-  const hvk_bf16* qkv;       // [T, 3C]
-  const hvk_bf16* dout;      // [T, C]   gradient of the attention core output
-  hvk_bf16* dqkv;            // [T, 3C]
-  const float* bias;         // [nH, R*R]
-  const float* scale;        // [nH]
-  float* dbias_acc;          // [nH, TAB] accumulator-order partial sums (zeroed by launcher)
-  float* dscale;             // [nH] (zeroed by launcher)
-  WmsaGeom g;
-};
 
 // Backward, one wave per (window, head), recomputing P from q, k (no saved
 // probabilities).  Phase A (query on the lane): S^T, P^T, dP^T = V dO^T,
@@ -363,6 +319,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
 #pragma unroll
     for (int ki = 0; ki < K::NT; ++ki) dbias[qi][ki] = hvk_f32x4{0, 0, 0, 0};
   float dscale = 0.f;
+  float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // this lane's column sums of dq
 
   for (int w = w0 + wave; w < w1; w += kWaves) {
     const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
@@ -505,7 +462,10 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
         for (int dt = 0; dt < 2; ++dt) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[qi];
+          for (int r = 0; r < 4; ++r) {
+            v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[qi];
+            dqb[dt][r] += v[r];
+          }
           hvk_st8(dst + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
         }
       }
@@ -584,27 +544,39 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
     atomicAdd(dst + e, v);
   }
   dscale = hvk_wave_sum(dscale);
-  if (lane == 0) atomicAdd(a.dscale + h, dscale);
+  if (lane == 0) atomicAdd(a.dscale_acc + h, dscale);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = hvk_row16_sum(dqb[dt][r]);
+      if (li == 0) atomicAdd(a.dqb_acc + h * 32 + 16 * dt + 4 * gq + r, v);
+    }
 }
 
-// Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R].
+// Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R], write
+// dscale / dq_bias, and leave the workspace zero for the next call.
 template <int WIN>
-__global__ __launch_bounds__(256) void wmsa_dbias_finalize_kernel(const float* __restrict__ acc,
-                                                                  float* __restrict__ dtab) {
+__global__ __launch_bounds__(256) void wmsa_finalize_kernel(BwdArgs a, float* __restrict__ dtab,
+                                                            float* __restrict__ dscale,
+                                                            float* __restrict__ dqb) {
   using K = WinCfg<WIN>;
   __shared__ float bins[K::R * K::R];
   const int h = blockIdx.x;
   for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) bins[i] = 0.f;
   __syncthreads();
+  float* acc = a.dbias_acc + (size_t)h * K::TAB;
   for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
     const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
     const int qi = blk / K::NT, ki = blk % K::NT;
     const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
     if (q < K::N && key < K::N) {
       const int idx = (q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1);
-      atomicAdd(&bins[idx], acc[(size_t)h * K::TAB + e]);
+      atomicAdd(&bins[idx], acc[e]);
     }
+    acc[e] = 0.f;
   }
+  finalize_scale_qb(a.dscale_acc, a.dqb_acc, dscale, dqb, h);
   __syncthreads();
   for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) dtab[(size_t)h * K::R * K::R + i] = bins[i];
 }
@@ -619,38 +591,18 @@ constexpr size_t bwd_lds_bytes() {
   return WinCfg<WIN>::TAB * 4 + kWaves * (size_t)(ROWS * 32 * 3 + ROWS * ROWS * 2) * 2;
 }
 
-// Persistent grid: n_heads * n_chunks <= `capacity` resident workgroups (no tail round),
-// n_chunks a multiple of 8 so every XCD group holds whole (chunk, all heads) sets.
-int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int capacity, WmsaGeom& g) {
-  if (B <= 0 || H <= 0 || W <= 0 || nH <= 0)
-    return hvk_set_error(HVK_EINVAL, "wmsa: bad shape B=%d H=%d W=%d nH=%d", B, H, W, nH);
-  if (C != 32 * nH)
-    return hvk_set_error(HVK_EUNSUPPORTED, "wmsa: head_dim must be 32 (C=%d, nH=%d)", C, nH);
-  if (H % win || W % win)
-    return hvk_set_error(HVK_EINVAL, "wmsa: H=%d W=%d not divisible by window %d", H, W, win);
-  if (shift < 0 || shift >= win)
-    return hvk_set_error(HVK_EINVAL, "wmsa: shift %d outside [0, %d)", shift, win);
-  g.B = B; g.H = H; g.W = W; g.C = C; g.nH = nH; g.shift = shift;
-  g.nWh = H / win; g.nWw = W / win;
-  g.n_windows = B * g.nWh * g.nWw;
-  int chunks = capacity / nH / 8 * 8;
-  if (chunks < 8) chunks = 8;
-  const int need = (g.n_windows + 7) / 8 * 8;  // never more chunks than windows (rounded)
-  g.n_chunks = chunks < need ? chunks : need;
-  return HVK_OK;
-}
 
 template <int WIN>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const int padded = a.g.n_chunks;  // already a multiple of 8
   const size_t lds = fwd_lds_bytes<WIN>();
-  hipLaunchKernelGGL(wmsa_fwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, wmsa_fwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd");
   return HVK_OK;
 }
 
 template <int WIN>
-int launch_bwd(const BwdArgs& a, float* dbias_table, hipStream_t st) {
+int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, hipStream_t st) {
   const int padded = a.g.n_chunks;  // already a multiple of 8
   const size_t lds = bwd_lds_bytes<WIN>();
   static bool attr_set = false;
@@ -659,11 +611,11 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(wmsa_bwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_bwd");
-  hipLaunchKernelGGL(wmsa_dbias_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st,
-                     a.dbias_acc, dbias_table);
-  HVK_CHECK_LAUNCH("wmsa_dbias_finalize");
+  hipLaunchKernelGGL(wmsa_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dbias_table,
+                     dscale, dqb);
+  HVK_CHECK_LAUNCH("wmsa_finalize");
   return HVK_OK;
 }
 
@@ -672,12 +624,20 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, hipStream_t st) {
 extern "C" {
 
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
-  const int n = window * window, nt = (n + 15) / 16;
-  return (size_t)num_heads * nt * nt * 256 * sizeof(float);
+  // [dbias accumulators][dscale nH][dq_bias 32 nH] floats
+  size_t acc;
+  if (hvk_wmsa::large_window(window)) {
+    acc = hvk_wmsa::large_acc_floats(num_heads, window);
+  } else {
+    const int n = window * window, nt = (n + 15) / 16;
+    acc = (size_t)num_heads * nt * nt * 256;
+  }
+  return (acc + (size_t)num_heads * 33) * sizeof(float);
 }
 
-int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale, int B,
-                 int H, int W, int C, int num_heads, int window, int shift, void* stream) {
+int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale,
+                 int B, int H, int W, int C, int num_heads, int window, int shift,
+                 void* stream) {
   if (!qkv || !out || !bias_table || !scale)
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_fwd: null pointer");
   FwdArgs a;
@@ -694,20 +654,22 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
   int rc = make_geom(B, H, W, C, num_heads, window, shift, cap, a.g);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (hvk_wmsa::large_window(window)) return hvk_wmsa::large_fwd(a, window, st);
   switch (window) {
     case 7: return launch_fwd<7>(a, st);
     case 8: return launch_fwd<8>(a, st);
     case 6: return launch_fwd<6>(a, st);
     case 4: return launch_fwd<4>(a, st);
     default:
-      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8)", window);
+      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8,12,16,24)", window);
   }
 }
 
-int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bias_table,
-                 const float* scale, float* dbias_table, float* dscale, float* workspace,
-                 size_t workspace_bytes, int B, int H, int W, int C, int num_heads, int window,
-                 int shift, void* stream) {
+int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
+                 const float* bias_table, const float* scale,
+                 float* dbias_table, float* dscale, float* workspace, size_t workspace_bytes,
+                 int B, int H, int W, int C, int num_heads, int window, int shift,
+                 void* stream) {
   if (!qkv || !dout || !dqkv || !bias_table || !scale || !dbias_table || !dscale || !workspace)
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: null pointer");
   if (workspace_bytes < hvk_wmsa_bwd_workspace_bytes(num_heads, window))
@@ -718,22 +680,24 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bia
   a.dqkv = static_cast<hvk_bf16*>(dqkv);
   a.bias = bias_table;
   a.scale = scale;
+  const size_t ws_acc = hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) -
+                        (size_t)num_heads * 33;
   a.dbias_acc = workspace;
-  a.dscale = dscale;
+  a.dscale_acc = workspace + ws_acc;
+  a.dqb_acc = a.dscale_acc + num_heads;
   // one resident 4-wave workgroup per CU (128 KB LDS, 1 wave/SIMD)
   int rc = make_geom(B, H, W, C, num_heads, window, shift, 256, a.g);
   if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(workspace, 0, hvk_wmsa_bwd_workspace_bytes(num_heads, window), st) != hipSuccess ||
-      hipMemsetAsync(dscale, 0, sizeof(float) * num_heads, st) != hipSuccess)
-    return hvk_set_error(HVK_EHIP, "hvk_wmsa_bwd: memset failed");
+  if (hvk_wmsa::large_window(window))
+    return hvk_wmsa::large_bwd(a, window, dbias_table, dscale, dq_bias, st);
   switch (window) {
-    case 7: return launch_bwd<7>(a, dbias_table, st);
-    case 8: return launch_bwd<8>(a, dbias_table, st);
-    case 6: return launch_bwd<6>(a, dbias_table, st);
-    case 4: return launch_bwd<4>(a, dbias_table, st);
+    case 7: return launch_bwd<7>(a, dbias_table, dscale, dq_bias, st);
+    case 8: return launch_bwd<8>(a, dbias_table, dscale, dq_bias, st);
+    case 6: return launch_bwd<6>(a, dbias_table, dscale, dq_bias, st);
+    case 4: return launch_bwd<4>(a, dbias_table, dscale, dq_bias, st);
     default:
-      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: window %d not built (4,6,7,8)", window);
+      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: window %d not built (4,6,7,8,12,16,24)", window);
   }
 }
 

@@ -1,0 +1,111 @@
+// Shared pieces of the W-MSA kernels (wmsa.hip: windows <= 8, wmsa_large.hip: 12/16/24).
+#pragma once
+#include "hvk_common.h"
+
+namespace hvk_wmsa {
+
+struct WmsaGeom {
+  int B, H, W, C, nH, shift;
+  int nWh, nWw, n_windows;   // windows per image row/col, total windows (B*nWh*nWw)
+  int n_chunks;              // window chunks per head (multiple of 8: XCD groups)
+};
+
+// token row (in the un-shifted [B*H*W] token order) of window position t
+__device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh, int ww, int win,
+                                                int t) {
+  int y = wh * win + t / win + g.shift;
+  int x = ww * win + t % win + g.shift;
+  if (y >= g.H) y -= g.H;
+  if (x >= g.W) x -= g.W;
+  return (b * g.H + y) * g.W + x;
+}
+
+// L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
+__device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post = 1.f) {
+  float f[8];
+  hvk_unpack8(v, f);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  ss = hvk_group4_sum(ss);
+  // F.normalize: x / max(||x||, eps) == x * rsqrt(max(||x||^2, eps^2))
+  rnorm = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
+  const float m = rnorm * post;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= m;
+  return hvk_pack8(f);
+}
+
+struct FwdArgs {
+  const hvk_bf16* qkv;       // [T, 3C]  x Wqkv^T + (q_bias, 0, 0)
+  hvk_bf16* out;             // [T, C]
+  const float* bias;         // [nH, R*R]   16*sigmoid(cpb)
+  const float* scale;        // [nH]        exp(clamp(logit_scale))
+  WmsaGeom g;
+};
+
+struct BwdArgs {
+  const hvk_bf16* qkv;       // [T, 3C]  x Wqkv^T + (q_bias, 0, 0)
+  const hvk_bf16* dout;      // [T, C]   gradient of the attention core output
+  hvk_bf16* dqkv;            // [T, 3C]
+  const float* bias;         // [nH, R*R]
+  const float* scale;        // [nH]
+  // workspace (zero on entry, re-zeroed by the finalize kernel):
+  float* dbias_acc;          // windows <= 8: [nH, TAB] accumulator-order partial sums;
+                             // large windows: [nH, R*R] bins
+  float* dscale_acc;         // [nH]
+  float* dqb_acc;            // [C]   column sums of dq (q_bias gradient)
+  WmsaGeom g;
+};
+
+// Persistent grid: n_heads * n_chunks <= `capacity` resident workgroups (no tail round),
+// n_chunks a multiple of 8 so every XCD group holds whole (chunk, all heads) sets.
+inline int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int capacity, WmsaGeom& g) {
+  if (B <= 0 || H <= 0 || W <= 0 || nH <= 0)
+    return hvk_set_error(HVK_EINVAL, "wmsa: bad shape B=%d H=%d W=%d nH=%d", B, H, W, nH);
+  if (C != 32 * nH)
+    return hvk_set_error(HVK_EUNSUPPORTED, "wmsa: head_dim must be 32 (C=%d, nH=%d)", C, nH);
+  if (H % win || W % win)
+    return hvk_set_error(HVK_EINVAL, "wmsa: H=%d W=%d not divisible by window %d", H, W, win);
+  if (shift < 0 || shift >= win)
+    return hvk_set_error(HVK_EINVAL, "wmsa: shift %d outside [0, %d)", shift, win);
+  g.B = B; g.H = H; g.W = W; g.C = C; g.nH = nH; g.shift = shift;
+  g.nWh = H / win; g.nWw = W / win;
+  g.n_windows = B * g.nWh * g.nWw;
+  int chunks = capacity / nH / 8 * 8;
+  if (chunks < 8) chunks = 8;
+  const int need = (g.n_windows + 7) / 8 * 8;  // never more chunks than windows (rounded)
+  g.n_chunks = chunks < need ? chunks : need;
+  return HVK_OK;
+}
+
+// large-window path (wmsa_large.hip): one workgroup per (window, head)
+bool large_window(int win);
+int large_fwd(const FwdArgs& a, int win, hipStream_t st);
+size_t large_acc_floats(int num_heads, int win);  // dbias_acc floats (bins)
+// backward + finalize: dbias_table [nH, R*R], dscale [nH], dq_bias [C] (may be null)
+int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,
+              hipStream_t st);
+
+// finalize helper: per head block, write dscale / dq_bias from the workspace and zero it
+__device__ __forceinline__ void finalize_scale_qb(float* dscale_acc, float* dqb_acc, float* dscale,
+                                                  float* dqb, int h) {
+  if (threadIdx.x < 32) {
+    const int c = h * 32 + threadIdx.x;
+    if (dqb) dqb[c] = dqb_acc[c];
+    dqb_acc[c] = 0.f;
+  }
+  if (threadIdx.x == 32) {
+    dscale[h] = dscale_acc[h];
+    dscale_acc[h] = 0.f;
+  }
+}
+
+// reduce v over the 16 lanes sharing lane>>4 (xor 1, 2, 4, 8)
+__device__ __forceinline__ float hvk_row16_sum(float v) {
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+}  // namespace hvk_wmsa

@@ -4,6 +4,8 @@ Every Function here launches only HIP kernels from libhvk.so on PyTorch's
 current stream; tensors are plumbing (PyTorch owns the memory).  There is no
 eager/CPU fallback: a CPU tensor or a missing library raises.
 """
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
@@ -11,25 +13,20 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 
-_TIMER = None  # list of (kind, start_event, end_event) while a bench timing window is open
+def kernel_timer_start(max_launches=8192):
+    """Time the next W-MSA launches inside libhvk (dispatch-packet events, include/hvk.h)."""
+    call("hvk_kernel_timer_enable", int(max_launches))
 
 
-def set_kernel_timer(timer):
-    """Open (list) / close (None) a timing window: every W-MSA launch is bracketed by HIP
-    events on the stream it is launched on (bench.py roofline)."""
-    global _TIMER
-    _TIMER = timer
-
-
-def _timed(kind, fn):
-    if _TIMER is None:
-        return fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    r = fn()
-    e.record()
-    _TIMER.append((kind, s, e))
-    return r
+def kernel_timer_stop():
+    """Stop timing; returns {"wmsa_fwd": (total_ms, launches), "wmsa_bwd": (...)}."""
+    out = {}
+    for kind, name in ((0, "wmsa_fwd"), (1, "wmsa_bwd")):
+        t, n = ctypes.c_double(0.0), ctypes.c_int(0)
+        call("hvk_kernel_timer_read", kind, ctypes.byref(t), ctypes.byref(n))
+        out[name] = (t.value, n.value)
+    call("hvk_kernel_timer_enable", 0)
+    return out
 
 
 def _bf16(t):
@@ -95,14 +92,31 @@ def linear(x, weight, bias=None):
 
 
 # --------------------------------------------------------------------------- W-MSA
+_WMSA_WS = {}
+
+
+def _wmsa_workspace(device, nbytes):
+    """Persistent zero-filled W-MSA backward workspace (the kernels leave it zero again,
+    include/hvk.h), one per device and size: no memset per call."""
+    key = (device, nbytes)
+    ws = _WMSA_WS.get(key)
+    if ws is None:
+        ws = torch.zeros(nbytes // 4, device=device, dtype=torch.float32)
+        _WMSA_WS[key] = ws
+    return ws
+
+
 class WindowAttentionCore(torch.autograd.Function):
     """Shifted-window cosine attention core on un-partitioned tokens.
 
-    qkv [B, H*W, 3C] bf16 -> out [B, H*W, C] bf16.  Stands in for
-    swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h)."""
+    qkv [B, H*W, 3C] bf16 (bias (q_bias, 0, 0) already in it) -> out [B, H*W, C] bf16,
+    without v_bias (the caller folds proj.weight @ v_bias into proj's bias).  Stands in for
+    swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h).  `q_bias` is taken only to
+    route its gradient: d loss / d q_bias = column sums of dq, produced by the backward
+    kernel (the qkv GEMM gets the bias detached, so no separate reduction runs)."""
 
     @staticmethod
-    def forward(ctx, qkv, bias_table, scale, H, W, num_heads, window, shift):
+    def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift):
         B, L, C3 = qkv.shape
         C = C3 // 3
         if L != H * W:
@@ -111,11 +125,11 @@ class WindowAttentionCore(torch.autograd.Function):
         bias_table = _f32(bias_table)
         scale = _f32(scale)
         out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
-        _timed("wmsa_fwd", lambda: call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(bias_table),
-                                        ptr(scale), B, H, W, C, num_heads, window, shift,
-                                        stream()))
+        call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(bias_table), ptr(scale), B, H, W, C,
+             num_heads, window, shift, stream())
         ctx.save_for_backward(qkv, bias_table, scale)
         ctx.geom = (B, H, W, C, num_heads, window, shift)
+        ctx.has_q_bias = q_bias is not None
         return out
 
     @staticmethod
@@ -126,17 +140,19 @@ class WindowAttentionCore(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         dtab = torch.empty_like(bias_table)
         dscale = torch.empty_like(scale)
+        dqb = (torch.empty(C, device=qkv.device, dtype=torch.float32)
+               if ctx.has_q_bias and ctx.needs_input_grad[1] else None)
         ws_bytes = _lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
-        ws = torch.empty(ws_bytes // 4, device=qkv.device, dtype=torch.float32)
-        _timed("wmsa_bwd", lambda: call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(dqkv),
-                                        ptr(bias_table), ptr(scale), ptr(dtab), ptr(dscale),
-                                        ptr(ws), ws_bytes, B, H, W, C, nh, win, shift,
-                                        stream()))
-        return dqkv, dtab, dscale, None, None, None, None, None
+        ws = _wmsa_workspace(qkv.device, ws_bytes)
+        call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(dqkv),
+             ptr(dqb) if dqb is not None else None, ptr(bias_table), ptr(scale), ptr(dtab),
+             ptr(dscale), ptr(ws), ws_bytes, B, H, W, C, nh, win, shift, stream())
+        return dqkv, dqb, dtab, dscale, None, None, None, None, None
 
 
-def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift):
-    return WindowAttentionCore.apply(qkv, bias_table, scale, H, W, num_heads, window, shift)
+def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift, q_bias=None):
+    return WindowAttentionCore.apply(qkv, q_bias, bias_table, scale, H, W, num_heads, window,
+                                     shift)
 
 
 # --------------------------------------------------------------------------- LayerNorm

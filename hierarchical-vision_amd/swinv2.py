@@ -176,18 +176,31 @@ class WindowAttention(nn.Module):
         """exp(clamp(logit_scale, max=ln 100)) as [nH] f32 (swinv2.py:230)."""
         return torch.clamp(self.logit_scale, max=self.logit_clamp_max).exp().reshape(-1).float()
 
-    def qkv_bias_vector(self):
+    def qkv_gemm_bias(self):
+        """Bias of the qkv GEMM: (q_bias, 0, 0), detached.  The reference's bias is
+        (q_bias, 0, v_bias) (swinv2.py:218-219); here q_bias's gradient comes out of the W-MSA
+        backward kernel (column sums of dq) and v_bias moves into proj_bias()."""
         if self.q_bias is None:
             return None
-        return torch.cat((self.q_bias, torch.zeros_like(self.v_bias, requires_grad=False), self.v_bias))
+        z = torch.zeros_like(self.q_bias, requires_grad=False)
+        return torch.cat((self.q_bias.detach(), z, z))
+
+    def proj_bias(self):
+        """proj.bias + proj.weight @ v_bias: softmax rows sum to 1, so P (V + v_bias) =
+        P V + v_bias and v_bias passes through proj as this constant (f32, exact)."""
+        if self.v_bias is None:
+            return self.proj.bias
+        with torch.autocast(device_type=self.v_bias.device.type, enabled=False):
+            return self.proj.bias + F.linear(self.v_bias.float(), self.proj.weight.float())
 
     def forward_tokens(self, x, H, W, shift, proj_bias=True):
         """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] after proj (without
-        proj's bias when proj_bias=False: the caller folds it into the next kernel)."""
-        qkv = ops.linear(x, self.qkv.weight, self.qkv_bias_vector())
+        proj's bias when proj_bias=False: the caller folds self.proj_bias() into the next
+        kernel)."""
+        qkv = ops.linear(x, self.qkv.weight, self.qkv_gemm_bias())
         o = ops.window_attention_core(qkv, self.bias_table(), self.scales(), H, W, self.num_heads,
-                                      self.window_size[0], shift)
-        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj.bias if proj_bias else None))
+                                      self.window_size[0], shift, q_bias=self.q_bias)
+        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj_bias() if proj_bias else None))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -260,7 +273,7 @@ class SwinTransformerBlock(nn.Module):
         a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold)
         dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
-                                        self.norm1.eps, abias=self.attn.proj.bias if fold else None)
+                                        self.norm1.eps, abias=self.attn.proj_bias() if fold else None)
         fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
         hid = self.mlp.hidden(xb)
         h = self.mlp.drop(ops.linear(hid, self.mlp.fc2.weight, None if fold else self.mlp.fc2.bias))

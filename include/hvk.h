@@ -30,26 +30,41 @@ extern "C" {
 int hvk_abi_version(void);
 const char* hvk_last_error_string(void);
 
+/* ---- Kernel timer (measurement only; bench.py's roofline) ---------------------------
+ * enable(n > 0): time the next n launches of the timed kernels (kind 0 = W-MSA forward,
+ * 1 = W-MSA backward main kernel) with start/stop events recorded by the dispatch packet
+ * itself (hipExtLaunchKernelGGL): a duration is the kernel's execution, as in a rocprofv3
+ * kernel trace.  enable(0) stops timing.  read() waits for the recorded launches of `kind`
+ * since the last enable and returns their summed duration (ms) and count. */
+int hvk_kernel_timer_enable(int max_launches);
+int hvk_kernel_timer_read(int kind, double* total_ms, int* launches);
+
 /* ---- Shifted-window cosine attention core ------------------------------------------
  * Replaces swinv2.py:399-412 (roll + window_partition), 221-261 (WindowAttention core:
  * normalize, q k^T, logit scale, CPB bias gather, shift mask, softmax, @v) and 420-429
  * (window_reverse + roll back).  qkv: bf16 [B*H*W, 3C] = F.linear output of swinv2.py:220
- * in UN-partitioned token order; out: bf16 [B*H*W, C] = input of proj (swinv2.py:262).
- * bias_table: f32 [num_heads, (2w-1)^2] = 16*sigmoid(cpb_mlp(relative_coords_table))
- * (swinv2.py:233-246 before the rpi gather); scale: f32 [num_heads] =
- * exp(clamp(logit_scale, max=ln 100)) (swinv2.py:230).  window/shift are the clamped
- * values of swinv2.py:328-331.  head_dim must be 32; window in {4, 6, 7, 8}. */
+ * in UN-partitioned token order, with bias (q_bias, 0, 0): v_bias does not enter, since
+ * softmax rows sum to 1 and P (V + v_bias) = P V + v_bias, which the caller folds into
+ * proj's bias (proj.bias + proj.weight v_bias).  out: bf16 [B*H*W, C] = input of proj
+ * (swinv2.py:262) minus v_bias.  bias_table: f32 [num_heads, (2w-1)^2] =
+ * 16*sigmoid(cpb_mlp(relative_coords_table)) (swinv2.py:233-246 before the rpi gather);
+ * scale: f32 [num_heads] = exp(clamp(logit_scale, max=ln 100)) (swinv2.py:230).
+ * window/shift are the clamped values of swinv2.py:328-331.  head_dim must be 32; window
+ * in {4, 6, 7, 8} (one wave per (window, head)) or {12, 16, 24} (one workgroup each). */
 int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale,
                  int B, int H, int W, int C, int num_heads, int window, int shift,
                  void* stream);
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
 /* dout: bf16 [B*H*W, C] (grad of `out`); dqkv: bf16 [B*H*W, 3C] (fully overwritten);
- * dbias_table: f32 [num_heads, (2w-1)^2] (overwritten); dscale: f32 [num_heads]
- * (overwritten, d loss / d scale). */
-int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, const float* bias_table,
-                 const float* scale, float* dbias_table, float* dscale, float* workspace,
-                 size_t workspace_bytes, int B, int H, int W, int C, int num_heads, int window,
-                 int shift, void* stream);
+ * dq_bias: f32 [C] (overwritten: column sums of the q part of dqkv = d loss / d q_bias,
+ * replacing the qkv bias-gradient reduction) or NULL; dbias_table: f32 [num_heads,
+ * (2w-1)^2] (overwritten); dscale: f32 [num_heads] (overwritten, d loss / d scale).
+ * workspace: f32, hvk_wmsa_bwd_workspace_bytes bytes, ALL ZERO on entry and left all zero
+ * on return (a caller keeps one zero-filled workspace: no memset per call). */
+int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
+                 const float* bias_table, const float* scale, float* dbias_table, float* dscale,
+                 float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
+                 int num_heads, int window, int shift, void* stream);
 
 /* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
  * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)

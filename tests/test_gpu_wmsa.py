@@ -11,6 +11,10 @@ CASES = [  # (B, H, W, heads, window, shift)
     (2, 14, 14, 2, 7, 3), (2, 14, 14, 2, 7, 0), (3, 56, 56, 3, 7, 3), (2, 28, 28, 6, 7, 3),
     (2, 7, 7, 24, 7, 0), (2, 16, 16, 2, 8, 4), (1, 12, 12, 4, 6, 3), (2, 8, 8, 2, 4, 2),
     (1, 21, 14, 3, 7, 3),
+    # large-window workgroup kernels (wmsa_large.hip): w12 (stage-3 clamp / pretrained 12),
+    # w16, w24 (SwinV2-B 384) shifted and unshifted
+    (1, 24, 24, 2, 12, 6), (2, 12, 12, 4, 12, 0), (1, 32, 32, 2, 16, 8),
+    (1, 48, 48, 2, 24, 12), (1, 24, 24, 3, 24, 0),
 ]
 
 
@@ -50,11 +54,14 @@ def test_wmsa_backward_matches_oracle(B, H, W, nh, win, shift):
     q_gpu = qkv.cuda().bfloat16().requires_grad_(True)
     t_gpu = tab.cuda().requires_grad_(True)
     s_gpu = scale.cuda().requires_grad_(True)
-    out = ops.window_attention_core(q_gpu, t_gpu, s_gpu, H, W, nh, win, shift)
+    # q_bias is already inside qkv; the op only routes its gradient (column sums of dq)
+    qb_gpu = torch.zeros(32 * nh, device="cuda", requires_grad=True)
+    out = ops.window_attention_core(q_gpu, t_gpu, s_gpu, H, W, nh, win, shift, q_bias=qb_gpu)
     out.backward(gout.cuda().bfloat16())
     torch.cuda.synchronize()
+    qb_ref = q_ref.grad[..., :32 * nh].sum(dim=(0, 1))
     for name, mine, ref in [("dqkv", q_gpu.grad, q_ref.grad), ("dbias", t_gpu.grad, t_ref.grad),
-                            ("dscale", s_gpu.grad, s_ref.grad)]:
+                            ("dscale", s_gpu.grad, s_ref.grad), ("dq_bias", qb_gpu.grad, qb_ref)]:
         mine = mine.float().cpu()
         rel = ((mine - ref).norm() / ref.norm().clamp_min(1e-12)).item()
         # dscale = sum(dS * cos) cancels (every dS row sums to 0), so bf16 rounding of

@@ -37,6 +37,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default=None, help="alternative libhvk build (tools/probe)")
+    ap.add_argument("--stage", type=int, default=None, help="only this stage (0-3)")
+    ap.add_argument("--only", choices=["fwd", "bwd"], default=None)
     args = ap.parse_args()
     from hvamd import _lib
     if args.lib:
@@ -44,7 +46,9 @@ def main():
     lib = _lib.load()
     tot_f = tot_b = 0.0
     byt_f = byt_b = 0
-    for name, B, H, W, C, nh, win, sh, nblk in STAGES:
+    for si, (name, B, H, W, C, nh, win, sh, nblk) in enumerate(STAGES):
+        if args.stage is not None and si != args.stage:
+            continue
         T = B * H * W
         qkv = torch.randn(T, 3 * C, device="cuda").bfloat16()
         out = torch.empty(T, C, device="cuda", dtype=torch.bfloat16)
@@ -54,8 +58,9 @@ def main():
         scale = torch.full((nh,), 10.0, device="cuda")
         dtab = torch.empty_like(tab)
         dsc = torch.empty_like(scale)
+        dqb = torch.empty(C, device="cuda")
         wsb = lib.hvk_wmsa_bwd_workspace_bytes(nh, win)
-        ws = torch.empty(wsb // 4, device="cuda")
+        ws = torch.zeros(wsb // 4, device="cuda")  # left zero by every call
         P = _lib.ptr
         st = _lib.stream
 
@@ -63,11 +68,11 @@ def main():
             _lib.call("hvk_wmsa_fwd", P(qkv), P(out), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
 
         def bwd():
-            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(dqkv), P(tab), P(scale), P(dtab), P(dsc),
+            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(dqkv), P(dqb), P(tab), P(scale), P(dtab), P(dsc),
                       P(ws), wsb, B, H, W, C, nh, win, sh, st())
 
-        tf = timeit(fwd, args.iters)
-        tb = timeit(bwd, args.iters)
+        tf = timeit(fwd, args.iters) if args.only != "bwd" else float("nan")
+        tb = timeit(bwd, args.iters) if args.only != "fwd" else float("nan")
         bf, bb = 8 * T * C, 16 * T * C
         tot_f += tf * nblk
         tot_b += tb * nblk
