@@ -1,0 +1,218 @@
+// Skinny MFMA GEMM for the memory-bound SwinV2 Linear layers on gfx950:
+//   Y[M, N] = X[M, K] W[N, K]^T (+ bias[N])      (nn.Linear / F.linear layout)
+// used for the forward (W = weight) and the input gradient (W = weight^T) of qkv / proj /
+// fc1 / fc2 / PatchMerging.reduction / PatchEmbed at the stages where K and N are small
+// (SwinV2-T stage 0-1: M = 200k-800k tokens, K, N <= 384).  Replaces F.linear of
+// swinv2.py:58-62, 220, 262, 492, 652 (as GEMM) for those shapes.
+//
+// These GEMMs are HBM-bound (arithmetic intensity K N / (K + N) <= 100 flop/B against a
+// machine balance of ~400), so the design streams X once and keeps W on chip:
+//  * a workgroup stages a BN x K block of W in LDS once and keeps it for its whole
+//    (persistent) life; the A operand of every MFMA is a W fragment read from LDS in a
+//    fragment-contiguous layout (one 1-KB conflict-free ds_read_b128 per MFMA);
+//  * Y^T = W X^T: the B operand is a 16-row tile of X read straight from HBM (16 B per
+//    lane), so X bytes are touched exactly once and no X staging is needed; the next
+//    tile's loads are issued before the current tile's MFMAs (software prefetch);
+//  * W rows are stored in LDS in a permuted order so that every lane ends up holding 8
+//    consecutive output columns of one row: each output row segment leaves as one 16-B
+//    store, bias added on the way (f32, from LDS).
+// v_mfma_f32_16x16x32_bf16, f32 accumulation, bf16 output (as F.linear under autocast).
+#include "hvk_common.h"
+
+namespace {
+
+constexpr int kWaves = 8;
+constexpr int kThreads = 64 * kWaves;
+
+template <int K, int BN>
+struct GCfg {
+  static_assert(K % 16 == 0 && BN % 32 == 0, "K multiple of 16, BN multiple of 32");
+  static constexpr int KS = (K + 31) / 32;   // MFMA k-steps (last one half-empty if K%32 == 16)
+  static constexpr int U4 = KS * 4;          // 16-B units per staged W row (zero padded)
+  static constexpr int NT = BN / 16;         // output-column tiles per workgroup
+  static constexpr bool PREF = KS <= 12;     // prefetch the next row tile's X fragments
+  static constexpr size_t LDS = (size_t)BN * U4 * 16 + (size_t)BN * 4;  // W block + bias
+};
+
+// LDS row p (= MFMA A row m = p%16 of tile t = p/16) holds W row n = perm(p): for the tile
+// pair (2j, 2j+1), A rows 4g + r of tile 2j + e hold n = 32j + 8g + 4e + r.  The MFMA
+// result D[4g + r][li] of tiles 2j, 2j+1 then gives lane (li, g) columns 32j + 8g .. +7.
+__device__ __forceinline__ int perm_row(int p) {
+  const int t = p >> 4, m = p & 15;
+  return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
+}
+
+template <int K, int BN, bool BIAS>
+__global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __restrict__ X,
+                                                          const hvk_bf16* __restrict__ W,
+                                                          const float* __restrict__ bias,
+                                                          hvk_bf16* __restrict__ Y, int M, int N,
+                                                          int ncb, int row_groups) {
+  using G = GCfg<K, BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* wl = reinterpret_cast<uint4*>(smem);                                // [NT][U4][16]
+  float* bl = reinterpret_cast<float*>(smem + (size_t)BN * G::U4 * 16);     // [BN]
+  // XCD-aware decode: the ncb column blocks of one row group share an XCD (L2) and walk
+  // the same row tiles in the same order
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int cb = loc % ncb, rg = (loc / ncb) * 8 + xcd;
+  if (rg >= row_groups) return;
+  const int n0 = cb * BN;
+
+  // stage W[n0 .. n0+BN) in the permuted, fragment-contiguous layout
+  for (int e = threadIdx.x; e < BN * G::U4; e += kThreads) {
+    const int p = e / G::U4, u = e % G::U4;
+    const int n = n0 + perm_row(p);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (8 * u < K) v = *reinterpret_cast<const uint4*>(W + (size_t)n * K + 8 * u);
+    wl[((p >> 4) * G::U4 + u) * 16 + (p & 15)] = v;
+  }
+  if (BIAS)
+    for (int e = threadIdx.x; e < BN; e += kThreads) bl[e] = bias[n0 + e];
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tiles = (M + 15) >> 4;
+  const int stride = row_groups * kWaves;
+  int tile = rg * kWaves + wave;
+
+  auto load_x = [&](int t, uint4 (&xf)[G::KS]) {
+    const int row = 16 * t + li;
+    const bool ok = t < tiles && row < M;
+    const hvk_bf16* xp = X + (size_t)row * K + 8 * g;
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) {
+      const bool in_k = (K % 32 == 0) || s + 1 < G::KS || g < 2;
+      xf[s] = (ok && in_k) ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  uint4 xf[G::KS];
+  load_x(tile, xf);
+  for (; tile < tiles; tile += stride) {
+    // W never changes, but re-read its fragments from LDS every tile: hoisting them out of
+    // the loop would pin KS x NT x 4 VGPRs (and spill)
+    asm volatile("" ::: "memory");
+    uint4 xn[G::KS];
+    if (G::PREF) load_x(tile + stride, xn);
+    hvk_f32x4 acc[G::NT];
+#pragma unroll
+    for (int t = 0; t < G::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s)
+#pragma unroll
+      for (int t = 0; t < G::NT; ++t)
+        acc[t] = hvk_mfma16(wl[(t * G::U4 + 4 * s + g) * 16 + li], xf[s], acc[t]);
+    const int row = 16 * tile + li;
+    if (row < M) {
+      hvk_bf16* yp = Y + (size_t)row * N + n0 + 8 * g;
+#pragma unroll
+      for (int j = 0; j < G::NT / 2; ++j) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * j][r];
+          v[4 + r] = acc[2 * j + 1][r];
+        }
+        if (BIAS) {
+          const float4 b0 = *reinterpret_cast<const float4*>(bl + 32 * j + 8 * g);
+          const float4 b1 = *reinterpret_cast<const float4*>(bl + 32 * j + 8 * g + 4);
+          v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+          v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        hvk_st16(yp + 32 * j, hvk_pack8(v));
+      }
+    }
+    if (G::PREF) {
+#pragma unroll
+      for (int s = 0; s < G::KS; ++s) xf[s] = xn[s];
+    } else {
+      load_x(tile + stride, xf);
+    }
+  }
+}
+
+int g_cu_count = 0;
+
+template <int K, int BN>
+int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
+                  int N, hipStream_t st) {
+  using G = GCfg<K, BN>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&linear_kernel<K, BN, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&linear_kernel<K, BN, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
+    attr = true;
+  }
+  if (!g_cu_count) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_linear: device query failed");
+    g_cu_count = prop.multiProcessorCount;
+  }
+  const int ncb = N / BN;
+  // resident workgroups per CU (LDS + VGPR limits): the persistent grid must all be resident
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&linear_kernel<K, BN, true>),
+                                                     kThreads, G::LDS) != hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = nb;
+  }
+  const int tiles = (M + 15) / 16;
+  int row_groups = g_cu_count * per_cu / ncb / 8 * 8;
+  const int need = (tiles + kWaves - 1) / kWaves;
+  if (row_groups > need) row_groups = (need + 7) / 8 * 8;
+  if (row_groups < 8) row_groups = 8;
+  const dim3 grid(row_groups * ncb);
+  if (bias)
+    hipLaunchKernelGGL((linear_kernel<K, BN, true>), grid, dim3(kThreads), G::LDS, st, X, W, bias,
+                       Y, M, N, ncb, row_groups);
+  else
+    hipLaunchKernelGGL((linear_kernel<K, BN, false>), grid, dim3(kThreads), G::LDS, st, X, W,
+                       bias, Y, M, N, ncb, row_groups);
+  HVK_CHECK_LAUNCH("hvk_linear");
+  return HVK_OK;
+}
+
+// (K, N) -> column block BN; 0 = not built (caller uses the library GEMM)
+int pick_bn(int K, int N) {
+  struct E { int K, N, BN; };
+  static const E table[] = {
+      {48, 96, 96},    {96, 96, 96},    {96, 288, 288},  {96, 384, 384},  {384, 96, 96},
+      {288, 96, 96},   {192, 192, 192}, {192, 576, 288}, {192, 768, 256}, {384, 192, 192},
+      {192, 384, 192},
+  };
+  for (const E& e : table)
+    if (e.K == K && e.N == N) return e.BN;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hvk_linear_supported(int M, int K, int N) { return M > 0 && pick_bn(K, N) > 0; }
+
+int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
+                   void* stream) {
+  if (!x || !w || !y) return hvk_set_error(HVK_EINVAL, "hvk_linear_fwd: null pointer");
+  if (M <= 0) return hvk_set_error(HVK_EINVAL, "hvk_linear_fwd: M=%d", M);
+  const int bn = pick_bn(K, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
+  const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
+  hvk_bf16* Y = static_cast<hvk_bf16*>(y);
+#define HVK_LIN(k, b) \
+  if (K == k && bn == b) return launch_linear<k, b>(X, W, bias, Y, M, N, st);
+  HVK_LIN(48, 96) HVK_LIN(96, 96) HVK_LIN(96, 288) HVK_LIN(96, 384) HVK_LIN(384, 96)
+  HVK_LIN(288, 96) HVK_LIN(192, 192) HVK_LIN(192, 288) HVK_LIN(192, 256) HVK_LIN(384, 192)
+#undef HVK_LIN
+  return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: shape K=%d N=%d not built", K, N);
+}
+
+}  // extern "C"

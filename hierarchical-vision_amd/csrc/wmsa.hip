@@ -102,6 +102,15 @@ __device__ __forceinline__ uint32_t mask_bits(uint32_t krow, uint32_t kcol, int 
   return (edge_r ? (krow ^ qr) : 0u) | (edge_c ? (kcol ^ qc) : 0u);
 }
 
+// Backward P / dS images [query][key] (ROWS bf16 per row = ROWS/4 8-B units): the 8-B unit
+// col8 of `row` is stored at col8 ^ f(row), f = (r0^r2) | r3<<1 | r1<<2: the 8-B writes of a
+// query tile and the transposed reads of phase B are then bank-conflict free.
+template <int ROWS>
+__device__ __forceinline__ int pimg_off(int row, int col8) {
+  const int f = ((row ^ (row >> 2)) & 1) | ((row >> 2) & 2) | ((row << 1) & 4);
+  return row * ROWS + (((col8 ^ f) & (ROWS / 4 - 1)) << 2);
+}
+
 // The forward's LDS image of V keeps head_dim columns in the order
 // col 16dt + 4g + r <-> d = 8g + 4dt + r, so an MFMA that reads them as A = X^T through
 // ds_read_b64_tr_b16 puts d = 8g..8g+7 of one token in lane (g, token) across its two
@@ -345,9 +354,10 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
     for (int i = 0; i < K::NT; ++i) {
       qf[i] = l2_normalize(qf[i], rnq[i]);
       kf[i] = l2_normalize(kf[i], rnk[i]);
-      *reinterpret_cast<uint4*>(qs + (16 * i + li) * 32 + 8 * gq) = qf[i];
-      *reinterpret_cast<uint4*>(ks + (16 * i + li) * 32 + 8 * gq) = kf[i];
-      *reinterpret_cast<uint4*>(dos + (16 * i + li) * 32 + 8 * gq) = df[i];
+      const int o16 = fm16(16 * i + li, gq) >> 1;  // bf16 elements
+      *reinterpret_cast<uint4*>(qs + o16) = qf[i];
+      *reinterpret_cast<uint4*>(ks + o16) = kf[i];
+      *reinterpret_cast<uint4*>(dos + o16) = df[i];
     }
     asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
     // K^T fragments for dQ^T = K^T dS^T (k = key, permuted order as in the forward)
@@ -356,8 +366,8 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
     for (int c = 0; c < K::NC; ++c)
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const hvk_bf16* base = ks + (32 * c + 4 * gq + (li >> 2)) * 32 + 16 * dt + 4 * (li & 3);
-        const uint2 lo = hvk_tr_read(base), hi = hvk_tr_read(base + 16 * 32);
+        const int rr = 32 * c + 4 * gq + (li >> 2), c8 = 4 * dt + (li & 3);
+        const uint2 lo = hvk_tr_read(ks + (fm8(rr, c8) >> 1)), hi = hvk_tr_read(ks + (fm8(rr + 16, c8) >> 1));
         kt_frag[c][dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
 
@@ -424,7 +434,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
           dscale += ds[ki][r] * s[ki][r];
         }
         // stage P and scale*dS as [query][key] rows for phase B
-        const int off = q * ROWS + 16 * ki + 4 * gq;
+        const int off = pimg_off<ROWS>(q, 4 * ki + gq);
         *reinterpret_cast<uint2*>(ps + off) =
             make_uint2(hvk_pack2(p[ki][0], p[ki][1]), hvk_pack2(p[ki][2], p[ki][3]));
         *reinterpret_cast<uint2*>(dss + off) =
@@ -448,7 +458,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       float qh[2][4], dot = 0.f;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const uint2 v = *reinterpret_cast<const uint2*>(qs + q * 32 + 16 * dt + 4 * gq);
+        const uint2 v = *reinterpret_cast<const uint2*>(qs + (fm8(q, 4 * dt + gq) >> 1));
         qh[dt][0] = hvk_lo(v.x); qh[dt][1] = hvk_hi(v.x);
         qh[dt][2] = hvk_lo(v.y); qh[dt][3] = hvk_hi(v.y);
 #pragma unroll
@@ -480,19 +490,18 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int c = 0; c < K::NC; ++c) {
         const int rq = 32 * c + 4 * gq + (li >> 2);
-        const hvk_bf16* pb = ps + rq * ROWS + 16 * kt + 4 * (li & 3);
-        const hvk_bf16* db = dss + rq * ROWS + 16 * kt + 4 * (li & 3);
-        uint2 lo = hvk_tr_read(pb), hi = hvk_tr_read(pb + 16 * ROWS);
+        const int plo = pimg_off<ROWS>(rq, 4 * kt + (li & 3)), phi = pimg_off<ROWS>(rq + 16, 4 * kt + (li & 3));
+        uint2 lo = hvk_tr_read(ps + plo), hi = hvk_tr_read(ps + phi);
         const uint4 pfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        lo = hvk_tr_read(db); hi = hvk_tr_read(db + 16 * ROWS);
+        lo = hvk_tr_read(dss + plo); hi = hvk_tr_read(dss + phi);
         const uint4 dsfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-          const hvk_bf16* ob = dos + rq * 32 + 16 * dt + 4 * (li & 3);
-          lo = hvk_tr_read(ob); hi = hvk_tr_read(ob + 16 * 32);
+          const int c8 = 4 * dt + (li & 3);
+          const int olo = fm8(rq, c8) >> 1, ohi = fm8(rq + 16, c8) >> 1;
+          lo = hvk_tr_read(dos + olo); hi = hvk_tr_read(dos + ohi);
           dv[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), pfr, dv[dt]);
-          const hvk_bf16* qb = qs + rq * 32 + 16 * dt + 4 * (li & 3);
-          lo = hvk_tr_read(qb); hi = hvk_tr_read(qb + 16 * 32);
+          lo = hvk_tr_read(qs + olo); hi = hvk_tr_read(qs + ohi);
           dk[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), dsfr, dk[dt]);
         }
       }
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       float kh[2][4], dot = 0.f;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const uint2 v = *reinterpret_cast<const uint2*>(ks + key * 32 + 16 * dt + 4 * gq);
+        const uint2 v = *reinterpret_cast<const uint2*>(ks + (fm8(key, 4 * dt + gq) >> 1));
         kh[dt][0] = hvk_lo(v.x); kh[dt][1] = hvk_hi(v.x);
         kh[dt][2] = hvk_lo(v.y); kh[dt][3] = hvk_hi(v.y);
 #pragma unroll

@@ -36,6 +36,21 @@ __device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post 
   return hvk_pack8(f);
 }
 
+// LDS images [rows][32] bf16 in "fragment-major" order: the 16-B unit (row, u) of a 16-row
+// tile sits at slot 16u + (row%16 ^ 12*(u&1)), so the natural MFMA operand read
+// (ds_read_b128, lane = row%16 + 16u), 16-B staging writes, 8-B row reads and the
+// transposed read (ds_read_b64_tr_b16) are all bank-conflict free (LDS bank model of
+// MI355X_MICROARCH.md, searched exhaustively).
+__device__ __forceinline__ int fm16(int row, int u) {  // byte offset of 16-B unit u of `row`
+  return ((row >> 4) * 64 + 16 * u + ((row & 15) ^ ((u & 1) * 12))) << 4;
+}
+__device__ __forceinline__ int fm8(int row, int col8) {  // byte offset of 8-B unit col8
+  return fm16(row, col8 >> 1) + ((col8 & 1) << 3);
+}
+__device__ __forceinline__ uint4 lds16(const char* img, int off) {
+  return *reinterpret_cast<const uint4*>(img + off);
+}
+
 struct FwdArgs {
   const hvk_bf16* qkv;       // [T, 3C]  x Wqkv^T + (q_bias, 0, 0)
   hvk_bf16* out;             // [T, C]

@@ -37,15 +37,6 @@ struct LCfg {
   static_assert(NT % WAVES == 0 || QB == 1, "tile split");
 };
 
-__device__ __forceinline__ int fm16(int row, int u) {  // byte offset of 16-B unit u of `row`
-  return ((row >> 4) * 64 + 16 * u + ((row & 15) ^ ((u & 1) * 12))) << 4;
-}
-__device__ __forceinline__ int fm8(int row, int col8) {  // byte offset of 8-B unit col8
-  return fm16(row, col8 >> 1) + ((col8 & 1) << 3);
-}
-__device__ __forceinline__ uint4 lds16(const char* img, int off) {
-  return *reinterpret_cast<const uint4*>(img + off);
-}
 // X^T fragment (A operand) of the 32-row chunk c, head-dim half dt, from an image of X
 __device__ __forceinline__ uint4 tr_frag(const char* img, int c, int dt, int li, int g) {
   const int rr = 32 * c + 4 * g + (li >> 2), c8 = 4 * dt + (li & 3);

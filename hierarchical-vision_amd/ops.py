@@ -63,15 +63,44 @@ def weight_grad(g, x):
     return part.sum(dim=0)
 
 
+_LIN_OK = {}
+
+
+def _linear_native(M, K, N):
+    """True when libhvk's skinny MFMA GEMM is built for (K, N) (include/hvk.h)."""
+    key = (K, N)
+    ok = _LIN_OK.get(key)
+    if ok is None:
+        ok = bool(_lib.load().hvk_linear_supported(max(M, 1), K, N))
+        _LIN_OK[key] = ok
+    return ok and M > 0
+
+
+def mm_nt(x2, wb, bias=None):
+    """y = x2 wb^T (+ bias): libhvk's MFMA kernel where built, else the library GEMM (the
+    compute-bound stage 2-3 shapes).  x2 [M, K] bf16, wb [N, K] bf16, bias f32 [N]."""
+    M, K = x2.shape
+    N = wb.shape[0]
+    if _linear_native(M, K, N):
+        y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
+        b = _f32(bias) if bias is not None else None
+        call("hvk_linear_fwd", ptr(x2), ptr(wb), ptr(b) if b is not None else None, ptr(y), M, K,
+             N, stream())
+        return y
+    return F.linear(x2, wb, bias.to(torch.bfloat16) if bias is not None else None)
+
+
 class LinearFn(torch.autograd.Function):
     """y = x W^T + b with bf16 operands (f32 master W, b); backward returns f32 dW / db
-    directly (no bf16 round trip), dW via the split-token batched GEMM."""
+    directly (no bf16 round trip), dW via the split-token batched GEMM.  Forward and input
+    gradient run on libhvk's skinny MFMA GEMM for the memory-bound shapes."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         xb = _bf16(x)
         wb = weight.to(torch.bfloat16)
-        y = F.linear(xb, wb, bias.to(torch.bfloat16) if bias is not None else None)
+        N, K = wb.shape
+        y = mm_nt(xb.reshape(-1, K), wb, bias).reshape(*xb.shape[:-1], N)
         ctx.save_for_backward(xb, wb)
         ctx.has_bias = bias is not None
         return y
@@ -81,7 +110,10 @@ class LinearFn(torch.autograd.Function):
         xb, wb = ctx.saved_tensors
         N, K = wb.shape
         g2 = _bf16(gy).reshape(-1, N)
-        gx = (g2 @ wb).reshape(xb.shape) if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = (mm_nt(g2, wb.t().contiguous()) if _linear_native(g2.shape[0], N, K)
+                  else g2 @ wb).reshape(xb.shape)
         dw = weight_grad(g2, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
         db = g2.sum(dim=0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, dw, db

@@ -66,6 +66,16 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
                  float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
                  int num_heads, int window, int shift, void* stream);
 
+/* ---- Skinny Linear (memory-bound GEMM) ------------------------------------------------
+ * y[M, N] = x[M, K] w[N, K]^T (+ bias[N]), bf16 in/out, f32 accumulation: F.linear of
+ * swinv2.py:58-62 (fc1/fc2), 220 (qkv), 262 (proj), 492 (PatchMerging.reduction) and
+ * 652 (patch embedding as GEMM) for the (K, N) shapes hvk_linear_supported() reports
+ * (SwinV2-T/B stages 0-1); with w = weight^T it is the input gradient of those layers.
+ * x: bf16 [M, K]; w: bf16 [N, K]; bias: f32 [N] or NULL; y: bf16 [M, N]. */
+int hvk_linear_supported(int M, int K, int N);
+int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
+                   void* stream);
+
 /* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
  * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)
  * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(proj(x))) with proj/fc2 run

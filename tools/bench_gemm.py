@@ -47,18 +47,35 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--tunable", default=None, help="enable PyTorch TunableOp, results file path")
+    ap.add_argument("--only", default=None, help="regex of gemm names to run")
     a = ap.parse_args()
+    if a.tunable:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(True)
+        torch.cuda.tunable.set_filename(a.tunable)
+        torch.cuda.tunable.set_max_tuning_duration(30)
     from hvamd import ops
     tot = {"fwd": 0.0, "dx": 0.0, "dw": 0.0}
     floor = {"fwd": 0.0, "dx": 0.0, "dw": 0.0}
-    print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw")
+    from hvamd import _lib
+    lib = _lib.load()
+    tot_h = 0.0
+    print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw | hvk fwd/dx us")
+    import re
     for name, M, K, N, cnt in shapes():
+        if a.only and not re.search(a.only, name):
+            continue
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
         dy = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
         tf = timeit(lambda: torch.mm(x, w.t()), a.iters)
         tx = timeit(lambda: torch.mm(dy, w), a.iters)
         tw = timeit(lambda: ops.weight_grad(dy, x), a.iters)
+        wt = w.t().contiguous()
+        hf = timeit(lambda: ops.mm_nt(x, w), a.iters) if lib.hvk_linear_supported(M, K, N) else tf
+        hx = timeit(lambda: ops.mm_nt(dy, wt), a.iters) if lib.hvk_linear_supported(M, N, K) else tx
+        tot_h += (hf + hx + tw) * cnt
         byt = 2 * (M * K + M * N + N * K)
         fl = 2 * M * N * K
         fl_us = max(byt / HBM, fl / MFMA) * 1e6
@@ -67,11 +84,12 @@ def main():
             tot[k] += t * cnt
             floor[k] += f * cnt / 1e3
         print(f"{name:10s} {M:7d} {K:5d} {N:6d} {cnt:2d} | {tf * 1e3:8.1f} {tx * 1e3:8.1f} {tw * 1e3:8.1f} | "
-              f"{fl_us:6.1f} {fl_us:6.1f} {fw_us:6.1f}", flush=True)
+              f"{fl_us:6.1f} {fl_us:6.1f} {fw_us:6.1f} | {hf * 1e3:7.1f} {hx * 1e3:7.1f}", flush=True)
         del x, w, dy
     for k in tot:
         print(f"total {k}: {tot[k]:.3f} ms/step (floor {floor[k]:.3f})")
-    print(f"all GEMMs: {sum(tot.values()):.3f} ms/step (floor {sum(floor.values()):.3f})")
+    print(f"all GEMMs: {sum(tot.values()):.3f} ms/step (floor {sum(floor.values()):.3f}); "
+          f"with hvk fwd/dx where built: {tot_h:.3f} ms/step")
 
 
 if __name__ == "__main__":
