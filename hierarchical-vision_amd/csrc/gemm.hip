@@ -17,12 +17,11 @@
 //    consecutive output columns of one row: each output row segment leaves as one 16-B
 //    store, bias added on the way (f32, from LDS).
 // v_mfma_f32_16x16x32_bf16, f32 accumulation, bf16 output (as F.linear under autocast).
+#include <stdlib.h>
+
 #include "hvk_common.h"
 
 namespace {
-
-constexpr int kWaves = 8;
-constexpr int kThreads = 64 * kWaves;
 
 template <int K, int BN>
 struct GCfg {
@@ -30,7 +29,6 @@ struct GCfg {
   static constexpr int KS = (K + 31) / 32;   // MFMA k-steps (last one half-empty if K%32 == 16)
   static constexpr int U4 = KS * 4;          // 16-B units per staged W row (zero padded)
   static constexpr int NT = BN / 16;         // output-column tiles per workgroup
-  static constexpr bool PREF = KS <= 12;     // prefetch the next row tile's X fragments
   static constexpr size_t LDS = (size_t)BN * U4 * 16 + (size_t)BN * 4;  // W block + bias
 };
 
@@ -42,13 +40,14 @@ __device__ __forceinline__ int perm_row(int p) {
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
-template <int K, int BN, bool BIAS>
-__global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __restrict__ X,
+template <int K, int BN, int WAVES, bool PREF, bool BIAS>
+__global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __restrict__ X,
                                                           const hvk_bf16* __restrict__ W,
                                                           const float* __restrict__ bias,
                                                           hvk_bf16* __restrict__ Y, int M, int N,
                                                           int ncb, int row_groups) {
   using G = GCfg<K, BN>;
+  constexpr int kThreads = 64 * WAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* wl = reinterpret_cast<uint4*>(smem);                                // [NT][U4][16]
   float* bl = reinterpret_cast<float*>(smem + (size_t)BN * G::U4 * 16);     // [BN]
@@ -73,8 +72,8 @@ __global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __rest
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tiles = (M + 15) >> 4;
-  const int stride = row_groups * kWaves;
-  int tile = rg * kWaves + wave;
+  const int stride = row_groups * WAVES;
+  int tile = rg * WAVES + wave;
 
   auto load_x = [&](int t, uint4 (&xf)[G::KS]) {
     const int row = 16 * t + li;
@@ -94,7 +93,7 @@ __global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __rest
     // the loop would pin KS x NT x 4 VGPRs (and spill)
     asm volatile("" ::: "memory");
     uint4 xn[G::KS];
-    if (G::PREF) load_x(tile + stride, xn);
+    if (PREF) load_x(tile + stride, xn);
     hvk_f32x4 acc[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
@@ -123,7 +122,7 @@ __global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __rest
         hvk_st16(yp + 32 * j, hvk_pack8(v));
       }
     }
-    if (G::PREF) {
+    if (PREF) {
 #pragma unroll
       for (int s = 0; s < G::KS; ++s) xf[s] = xn[s];
     } else {
@@ -134,17 +133,24 @@ __global__ __launch_bounds__(kThreads) void linear_kernel(const hvk_bf16* __rest
 
 int g_cu_count = 0;
 
-template <int K, int BN>
+template <int K, int BN, int WAVES, bool PREF>
 int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
                   int N, hipStream_t st) {
   using G = GCfg<K, BN>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&linear_kernel<K, BN, true>),
+  constexpr int kThreads = 64 * WAVES;
+  auto kb = &linear_kernel<K, BN, WAVES, PREF, true>;
+  auto kn = &linear_kernel<K, BN, WAVES, PREF, false>;
+  static int per_cu = 0;  // resident workgroups per CU (LDS + VGPR limits), queried once
+  if (!per_cu) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&linear_kernel<K, BN, false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kn),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)G::LDS);
-    attr = true;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kb),
+                                                     kThreads, G::LDS) != hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = nb;
   }
   if (!g_cu_count) {
     int dev = 0;
@@ -154,65 +160,78 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
     g_cu_count = prop.multiProcessorCount;
   }
   const int ncb = N / BN;
-  // resident workgroups per CU (LDS + VGPR limits): the persistent grid must all be resident
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&linear_kernel<K, BN, true>),
-                                                     kThreads, G::LDS) != hipSuccess || nb < 1)
-      nb = 1;
-    per_cu = nb;
-  }
+  // persistent grid: every workgroup resident (it loops over row tiles)
   const int tiles = (M + 15) / 16;
   int row_groups = g_cu_count * per_cu / ncb / 8 * 8;
-  const int need = (tiles + kWaves - 1) / kWaves;
+  const int need = (tiles + WAVES - 1) / WAVES;
   if (row_groups > need) row_groups = (need + 7) / 8 * 8;
   if (row_groups < 8) row_groups = 8;
   const dim3 grid(row_groups * ncb);
   if (bias)
-    hipLaunchKernelGGL((linear_kernel<K, BN, true>), grid, dim3(kThreads), G::LDS, st, X, W, bias,
-                       Y, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, M, N, ncb, row_groups);
   else
-    hipLaunchKernelGGL((linear_kernel<K, BN, false>), grid, dim3(kThreads), G::LDS, st, X, W,
-                       bias, Y, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, M, N, ncb, row_groups);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }
 
-// (K, N) -> column block BN; 0 = not built (caller uses the library GEMM)
-int pick_bn(int K, int N) {
-  struct E { int K, N, BN; };
-  static const E table[] = {
-      {48, 96, 96},    {96, 96, 96},    {96, 288, 288},  {96, 384, 384},  {384, 96, 96},
-      {288, 96, 96},   {192, 192, 192}, {192, 576, 288}, {192, 768, 256}, {384, 192, 192},
-      {192, 384, 192},
-  };
-  for (const E& e : table)
-    if (e.K == K && e.N == N) return e.BN;
-  return 0;
+struct LinCfg {
+  int K, N, BN, waves, pref;
+};
+// built configurations; variant 0 is the default, HVK_LINEAR_VARIANT picks another row
+// of the same (K, N) for experiments (tools/bench_gemm.py)
+const LinCfg kLin[][4] = {
+    //  default               16 waves               16 waves, no pref       half BN
+    {{48, 96, 96, 8, 1}, {48, 96, 96, 16, 1}, {48, 96, 96, 16, 0}, {48, 96, 96, 8, 1}},
+    {{96, 96, 96, 8, 1}, {96, 96, 96, 16, 1}, {96, 96, 96, 16, 0}, {96, 96, 96, 8, 1}},
+    {{96, 288, 288, 8, 1}, {96, 288, 288, 16, 1}, {96, 288, 288, 16, 0}, {96, 288, 96, 16, 1}},
+    {{96, 384, 384, 8, 1}, {96, 384, 384, 16, 1}, {96, 384, 384, 16, 0}, {96, 384, 192, 16, 1}},
+    {{384, 96, 96, 8, 1}, {384, 96, 96, 16, 1}, {384, 96, 96, 16, 0}, {384, 96, 96, 8, 0}},
+    {{288, 96, 96, 8, 1}, {288, 96, 96, 16, 1}, {288, 96, 96, 16, 0}, {288, 96, 96, 8, 0}},
+    {{192, 192, 192, 8, 1}, {192, 192, 192, 16, 1}, {192, 192, 192, 16, 0}, {192, 192, 96, 16, 1}},
+    {{192, 576, 288, 8, 1}, {192, 576, 288, 16, 1}, {192, 576, 288, 16, 0}, {192, 576, 192, 16, 1}},
+    {{192, 768, 256, 8, 1}, {192, 768, 256, 16, 1}, {192, 768, 256, 16, 0}, {192, 768, 192, 16, 1}},
+    {{384, 192, 192, 8, 1}, {384, 192, 192, 16, 1}, {384, 192, 192, 16, 0}, {384, 192, 96, 16, 1}},
+};
+
+const LinCfg* pick(int K, int N) {
+  static const int variant = [] {
+    const char* e = getenv("HVK_LINEAR_VARIANT");
+    const int v = e ? atoi(e) : 0;
+    return v >= 0 && v < 4 ? v : 0;
+  }();
+  for (const auto& row : kLin)
+    if (row[0].K == K && row[0].N == N) return &row[variant];
+  return nullptr;
 }
 
 }  // namespace
 
 extern "C" {
 
-int hvk_linear_supported(int M, int K, int N) { return M > 0 && pick_bn(K, N) > 0; }
+int hvk_linear_supported(int M, int K, int N) { return M > 0 && pick(K, N) != nullptr; }
 
 int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
                    void* stream) {
   if (!x || !w || !y) return hvk_set_error(HVK_EINVAL, "hvk_linear_fwd: null pointer");
   if (M <= 0) return hvk_set_error(HVK_EINVAL, "hvk_linear_fwd: M=%d", M);
-  const int bn = pick_bn(K, N);
+  const LinCfg* c = pick(K, N);
+  if (!c) return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: shape K=%d N=%d not built", K, N);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
   const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
   hvk_bf16* Y = static_cast<hvk_bf16*>(y);
-#define HVK_LIN(k, b) \
-  if (K == k && bn == b) return launch_linear<k, b>(X, W, bias, Y, M, N, st);
-  HVK_LIN(48, 96) HVK_LIN(96, 96) HVK_LIN(96, 288) HVK_LIN(96, 384) HVK_LIN(384, 96)
-  HVK_LIN(288, 96) HVK_LIN(192, 192) HVK_LIN(192, 288) HVK_LIN(192, 256) HVK_LIN(384, 192)
+#define HVK_LIN(k, bn, wv, pf)                                         \
+  if (c->K == k && c->BN == bn && c->waves == wv && c->pref == pf)     \
+    return launch_linear<k, bn, wv, pf>(X, W, bias, Y, M, N, st);
+#define HVK_LIN3(k, bn) HVK_LIN(k, bn, 8, 1) HVK_LIN(k, bn, 16, 1) HVK_LIN(k, bn, 16, 0)
+  HVK_LIN3(48, 96) HVK_LIN3(96, 96) HVK_LIN3(96, 288) HVK_LIN3(96, 384) HVK_LIN3(384, 96)
+  HVK_LIN3(288, 96) HVK_LIN3(192, 192) HVK_LIN3(192, 288) HVK_LIN3(192, 256) HVK_LIN3(384, 192)
+  HVK_LIN(96, 192, 16, 1) HVK_LIN(384, 96, 8, 0) HVK_LIN(288, 96, 8, 0) HVK_LIN(192, 96, 16, 1)
+  HVK_LIN(384, 96, 16, 1)
+#undef HVK_LIN3
 #undef HVK_LIN
-  return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: shape K=%d N=%d not built", K, N);
+  return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);
 }
 
 }  // extern "C"

@@ -168,19 +168,10 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
       const int t = 16 * i + li;
       row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
       if (t < K::N) {
-#ifdef HVK_PROBE_CONTIGUOUS  // tools/probe: same byte count, fully contiguous 1-KB wave reads
-        const size_t nblk = (size_t)g.B * g.H * g.W * 3 * C / 1536;
-        const size_t blk = ((size_t)(w * g.nH + h) * K::NT + i) % nblk;
-        const hvk_bf16* p = a.qkv + blk * 1536 + 8 * lane;
-        qf[i] = *reinterpret_cast<const uint4*>(p);
-        kf[i] = *reinterpret_cast<const uint4*>(p + 512);
-        vf[i] = *reinterpret_cast<const uint4*>(p + 1024);
-#else
         const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
         qf[i] = hvk_ld16(p);
         kf[i] = hvk_ld16(p + C);
         vf[i] = hvk_ld16(p + 2 * C);
-#endif
       } else {
         qf[i] = kf[i] = vf[i] = make_uint4(0, 0, 0, 0);
       }
@@ -192,12 +183,7 @@ __global__ __launch_bounds__(kThreads, 4) void wmsa_fwd_kernel(FwdArgs a) {
         uint4 t = qf[i];
         t.x ^= kf[i].x ^ vf[i].x; t.y ^= kf[i].y ^ vf[i].y;
         t.z ^= kf[i].z ^ vf[i].z; t.w ^= kf[i].w ^ vf[i].w;
-#ifdef HVK_PROBE_CONTIGUOUS_STORE
-        const size_t nb = (size_t)g.B * g.H * g.W * C / 512;
-        *reinterpret_cast<uint4*>(a.out + (((size_t)(w * g.nH + h) * K::NT + i) % nb) * 512 + 8 * lane) = t;
-#else
         *reinterpret_cast<uint4*>(a.out + (size_t)row[i] * C + h * 32 + 8 * gq) = t;
-#endif
       }
     continue;
 #endif
