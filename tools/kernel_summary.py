@@ -1,6 +1,7 @@
 """Group a `rocprofv3 --kernel-trace` trace into per-step categories.
 
     python tools/kernel_summary.py gpurun_out/prof/run_results.db --anchor hxe_fwd --skip 3
+    python tools/kernel_summary.py gpurun_out/prof/run_kernel_trace.csv --anchor hxe_fwd --skip 3
     python tools/kernel_summary.py gpurun_out/prof/.../kernel_stats.csv --steps 15
 
 With a rocpd .db, --anchor/--skip keep only the dispatches from the (skip+1)-th launch of
@@ -19,6 +20,7 @@ CATS = [  # (category, regex on the kernel name), first match wins
     ("bias_gelu", r"bias_gelu|colsum_rows"),
     ("patch_merge", r"merge_kernel"),
     ("losses", r"multitask|hxe"),
+    ("gemm(hvk)", r"linear_kernel"),
     ("gemm", r"Cijk|gemm|Gemm|GEMM|mfma|MT\d+x\d+"),
     ("memset", r"[Mm]emset|fill"),
     ("reduce", r"reduce|Reduce"),
@@ -35,9 +37,14 @@ def main():
     ap.add_argument("--anchor", default=None, help="regex of a once-per-step kernel (.db only)")
     ap.add_argument("--skip", type=int, default=0, help="anchor launches to drop (warmup)")
     a = ap.parse_args()
-    if a.csv.endswith(".db"):
-        db = sqlite3.connect(a.csv)
-        disp = db.execute("select name, start, end from kernels order by start").fetchall()
+    if a.csv.endswith(".db") or a.csv.endswith("kernel_trace.csv"):
+        if a.csv.endswith(".db"):
+            db = sqlite3.connect(a.csv)
+            disp = db.execute("select name, start, end from kernels order by start").fetchall()
+        else:
+            disp = sorted((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                          for r in csv.DictReader(open(a.csv)))
+            disp.sort(key=lambda d: d[1])
         if a.anchor:
             starts = [st for n, st, _ in disp if re.search(a.anchor, n)]
             t0 = starts[a.skip]
