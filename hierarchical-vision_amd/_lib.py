@@ -27,6 +27,8 @@ SIGNATURES = {
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
     "hvk_linear_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),

@@ -40,11 +40,15 @@ __device__ __forceinline__ int perm_row(int p) {
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
-template <int K, int BN, int WAVES, bool PREF, bool BIAS>
+// EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
+// bf16 pre-activation kept for the backward and the activation for fc2 (the reference's
+// F.linear(+bias) -> nn.GELU on the bf16 tensor, swinv2.py:58-62).
+template <int K, int BN, int WAVES, bool PREF, bool BIAS, int EPI = 0>
 __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __restrict__ X,
                                                           const hvk_bf16* __restrict__ W,
                                                           const float* __restrict__ bias,
-                                                          hvk_bf16* __restrict__ Y, int M, int N,
+                                                          hvk_bf16* __restrict__ Y,
+                                                          hvk_bf16* __restrict__ Y2, int M, int N,
                                                           int ncb, int row_groups) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
@@ -119,7 +123,15 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
           v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
-        hvk_st16(yp + 32 * j, hvk_pack8(v));
+        const uint4 hv = hvk_pack8(v);
+        hvk_st16(yp + 32 * j, hv);
+        if (EPI == 1) {
+          float u[8];
+          hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
+#pragma unroll
+          for (int e = 0; e < 8; ++e) u[e] = hvk_gelu::gelu(u[e]);
+          hvk_st16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j, hvk_pack8(u));
+        }
       }
     }
     if (PREF) {
@@ -133,13 +145,13 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
 
 int g_cu_count = 0;
 
-template <int K, int BN, int WAVES, bool PREF>
+template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
 int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
-                  int N, hipStream_t st) {
+                  int N, hipStream_t st, hvk_bf16* Y2 = nullptr) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
-  auto kb = &linear_kernel<K, BN, WAVES, PREF, true>;
-  auto kn = &linear_kernel<K, BN, WAVES, PREF, false>;
+  auto kb = &linear_kernel<K, BN, WAVES, PREF, true, EPI>;
+  auto kn = &linear_kernel<K, BN, WAVES, PREF, false, EPI>;
   static int per_cu = 0;  // resident workgroups per CU (LDS + VGPR limits), queried once
   if (!per_cu) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kb),
@@ -168,9 +180,9 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   if (row_groups < 8) row_groups = 8;
   const dim3 grid(row_groups * ncb);
   if (bias)
-    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups);
   else
-    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }
@@ -232,6 +244,26 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
 #undef HVK_LIN3
 #undef HVK_LIN
   return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);
+}
+
+int hvk_linear_gelu_supported(int M, int K, int N) {
+  const LinCfg* c = pick(K, N);
+  return M > 0 && c && ((c->K == 96 && c->BN == 384) || (c->K == 192 && c->BN == 256)) &&
+         c->waves == 8 && c->pref == 1;
+}
+
+int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
+                        int K, int N, void* stream) {
+  if (!x || !w || !h || !y) return hvk_set_error(HVK_EINVAL, "hvk_linear_gelu_fwd: null pointer");
+  if (!hvk_linear_gelu_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_gelu_fwd: shape M=%d K=%d N=%d not built", M, K, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
+  const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
+  hvk_bf16* H = static_cast<hvk_bf16*>(h);
+  hvk_bf16* Yg = static_cast<hvk_bf16*>(y);
+  if (K == 96) return launch_linear<96, 384, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+  return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
 }
 
 }  // extern "C"

@@ -106,6 +106,17 @@ __device__ __forceinline__ void hvk_st8(void* p, uint2 v) {
 #endif
 }
 
+// ---- GELU, exact erf form (nn.GELU(), swinv2.py:60): shared by the activation kernels
+// and the fused fc1 epilogue so both paths round identically
+namespace hvk_gelu {
+constexpr float kInvSqrt2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erff(u * kInvSqrt2)); }
+__device__ __forceinline__ float gelu_grad(float u) {
+  return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
+}
+}  // namespace hvk_gelu
+
 // ---- MFMA 16x16x32 bf16 -> f32 --------------------------------------------
 // A lane l holds A[row l&15][k = 8(l>>4) + j], B lane l holds B[k = 8(l>>4) + j][col l&15],
 // D lane l holds D[row 4(l>>4) + r][col l&15], r = 0..3.

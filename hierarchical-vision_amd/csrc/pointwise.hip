@@ -12,13 +12,9 @@
 namespace {
 
 constexpr int kWaves = 4;
-constexpr float kInvSqrt2 = 0.70710678118654752f;
-constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+using hvk_gelu::gelu;
+using hvk_gelu::gelu_grad;
 
-__device__ __forceinline__ float gelu(float u) { return 0.5f * u * (1.f + erff(u * kInvSqrt2)); }
-__device__ __forceinline__ float gelu_grad(float u) {
-  return 0.5f * (1.f + erff(u * kInvSqrt2)) + u * kInvSqrt2Pi * __expf(-0.5f * u * u);
-}
 
 __global__ __launch_bounds__(64 * kWaves) void bias_gelu_fwd_kernel(const hvk_bf16* __restrict__ h,
                                                                     const float* __restrict__ b,

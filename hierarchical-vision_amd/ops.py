@@ -52,7 +52,9 @@ def _split_k_chunks(rows):
 def weight_grad(g, x):
     """dW = g^T x in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to ~10^6) and
     N, K small: the library picks ~50 workgroups for this shape, so split the token
-    reduction into a batched GEMM over chunks (thousands of workgroups) + a small sum."""
+    reduction into a batched GEMM over chunks (thousands of workgroups) + a small sum.
+    (A token-sliced MFMA kernel with f32 atomics was measured slower on every SwinV2-T shape:
+    with one 32-token chunk in flight per workgroup it is HBM-latency bound)"""
     M = g.shape[0]
     nc = _split_k_chunks(M)
     if nc == 1:
@@ -272,6 +274,54 @@ class BiasGelu(torch.autograd.Function):
 
 def bias_gelu(h, bias):
     return BiasGelu.apply(h, bias)
+
+
+class LinearGelu(torch.autograd.Function):
+    """y = GELU(x W^T + b) as ONE kernel (hvk_linear_gelu_fwd: fc1 GEMM with the bias + GELU
+    epilogue, writing the bf16 pre-activation h for the backward); backward = the activation
+    backward on h (db = its column sums) + the Linear backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        xb = _bf16(x)
+        wb = weight.to(torch.bfloat16)
+        N, K = wb.shape
+        x2 = xb.reshape(-1, K)
+        M = x2.shape[0]
+        h = torch.empty((M, N), device=x.device, dtype=torch.bfloat16)
+        y = torch.empty_like(h)
+        call("hvk_linear_gelu_fwd", ptr(x2), ptr(wb), ptr(_f32(bias)), ptr(h), ptr(y), M, K, N,
+             stream())
+        ctx.save_for_backward(xb, wb, h)
+        return y.reshape(*xb.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb, h = ctx.saved_tensors
+        N, K = wb.shape
+        g2 = _bf16(gy).reshape(-1, N)
+        M = g2.shape[0]
+        gh = torch.empty_like(h)
+        db = torch.empty(N, device=h.device, dtype=torch.float32)
+        ws_bytes = _lib.load().hvk_bias_gelu_bwd_workspace_bytes(N)
+        ws = torch.empty(ws_bytes // 4, device=h.device, dtype=torch.float32)
+        call("hvk_bias_gelu_bwd", ptr(h), None, ptr(g2), ptr(gh), ptr(db), ptr(ws), ws_bytes, M, N,
+             stream())
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = (mm_nt(gh, wb.t().contiguous()) if _linear_native(M, N, K)
+                  else gh @ wb).reshape(xb.shape)
+        dw = weight_grad(gh, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
+        return gx, dw, db
+
+
+def linear_gelu(x, weight, bias):
+    """GELU(F.linear(x, weight, bias)): fused kernel where built, else GEMM + activation kernel."""
+    K = weight.shape[1]
+    M = x.numel() // K
+    if bias is not None and _lib.load().hvk_linear_gelu_supported(M, K, weight.shape[0]):
+        return LinearGelu.apply(x, weight, bias)
+    return bias_gelu(linear(x, weight), bias)
 
 
 # --------------------------------------------------------------------------- PatchMerging

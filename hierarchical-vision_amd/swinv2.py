@@ -122,7 +122,7 @@ class Mlp(nn.Module):
         """GELU(fc1(x)) with the bias add fused into the activation kernel."""
         if not isinstance(self.act, nn.GELU) or self.act.approximate != "none":
             return self.drop(self.act(ops.linear(x, self.fc1.weight, self.fc1.bias)))
-        return self.drop(ops.bias_gelu(ops.linear(x, self.fc1.weight), self.fc1.bias))
+        return self.drop(ops.linear_gelu(x, self.fc1.weight, self.fc1.bias))
 
 
 class WindowAttention(nn.Module):

@@ -75,6 +75,12 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
 int hvk_linear_supported(int M, int K, int N);
 int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
                    void* stream);
+/* fc1 with its activation fused (swinv2.py:58-62): h = bf16(x w^T + bias) (kept for the
+ * backward, = the reference's fc1 output) and y = GELU(h) (exact erf, bf16); replaces
+ * hvk_linear_fwd + hvk_bias_gelu_fwd where hvk_linear_gelu_supported(). */
+int hvk_linear_gelu_supported(int M, int K, int N);
+int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
+                        int K, int N, void* stream);
 
 /* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
  * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)

@@ -43,3 +43,27 @@ def test_linear_autograd_uses_native_and_matches():
     for mine, ref in [(y.float(), yr), (x.grad.float(), xr.grad), (w.grad, wr.grad), (b.grad, br.grad)]:
         rel = ((mine - ref).norm() / ref.norm()).item()
         assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("K,N", [(96, 384), (192, 768)])
+def test_linear_gelu_fused_matches_fp32(K, N):
+    from hvamd import _lib, ops
+    M = 3000
+    assert _lib.load().hvk_linear_gelu_supported(M, K, N)
+    gen = torch.Generator(device="cuda").manual_seed(K + N)
+    x = torch.randn(M, K, device="cuda", generator=gen).bfloat16().requires_grad_(True)
+    w = (torch.randn(N, K, device="cuda", generator=gen) / K ** 0.5).requires_grad_(True)
+    b = torch.randn(N, device="cuda", generator=gen).requires_grad_(True)
+    y = ops.linear_gelu(x, w, b)
+    gy = torch.randn(M, N, device="cuda", generator=gen)
+    y.backward(gy.bfloat16())
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = torch.nn.functional.gelu(xr @ wr.t() + br)
+    yr.backward(gy.bfloat16().float())
+    torch.cuda.synchronize()
+    for name, mine, ref in [("y", y.float(), yr), ("dx", x.grad.float(), xr.grad),
+                            ("dw", w.grad, wr.grad), ("db", b.grad, br.grad)]:
+        rel = ((mine - ref).norm() / ref.norm()).item()
+        assert rel < 1e-2, (name, rel)
