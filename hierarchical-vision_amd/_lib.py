@@ -27,6 +27,10 @@ SIGNATURES = {
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
     "hvk_linear_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_cpb_fwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p]),
+    "hvk_cpb_bwd_workspace_bytes": (_sz, [_i, _i]),
+    "hvk_cpb_bwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
+                         _p]),
     "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),

@@ -120,6 +120,8 @@ struct LnBwd {
   const float* mean; const float* rstd; const float* gx; const hvk_bf16* gxb;
   int rows, C, rows_per_sample;
   float* gx0; hvk_bf16* ga; float* part;  // part: [gridDim.x][3][C] dgamma / dbeta / dabias
+  float* zero0; float* zero1; float* zero2;  // [C] outputs of the colsum kernel that follows:
+                                             // zeroed here (stream order) instead of memsets
 };
 
 template <int EPT, int TPR>
@@ -130,6 +132,12 @@ __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
   const int sub = lane / TPR, t = lane % TPR;
   const int c0 = t * EPT;
   const bool act = c0 < p.C;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < p.C; i += blockDim.x) {
+      p.zero0[i] = 0.f;
+      p.zero1[i] = 0.f;
+      if (p.zero2) p.zero2[i] = 0.f;
+    }
   float gm[EPT], ab[EPT], dg[EPT], db[EPT], dab[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) { gm[j] = ab[j] = dg[j] = db[j] = dab[j] = 0.f; }
@@ -305,13 +313,9 @@ int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
   if (grid > kBwdBlocks) grid = kBwdBlocks;
   LnBwd p{static_cast<const hvk_bf16*>(a), abias, gamma, sample_scale, mean, rstd, gx,
           static_cast<const hvk_bf16*>(gxb), rows, C, rows_per_sample, gx0,
-          static_cast<hvk_bf16*>(ga), workspace};
+          static_cast<hvk_bf16*>(ga), workspace, dgamma, dbeta, dabias};
   HVK_LN_DISPATCH(ln_bwd_kernel, dim3(grid), st, p);
   HVK_CHECK_LAUNCH("ln_bwd");
-  if (hipMemsetAsync(dgamma, 0, sizeof(float) * C, st) != hipSuccess ||
-      hipMemsetAsync(dbeta, 0, sizeof(float) * C, st) != hipSuccess ||
-      (dabias && hipMemsetAsync(dabias, 0, sizeof(float) * C, st) != hipSuccess))
-    return hvk_set_error(HVK_EHIP, "hvk_ln_residual_bwd: memset failed");
   hipLaunchKernelGGL(colsum_kernel, dim3((3 * C + 63) / 64, kRedRowGroups), dim3(64), 0, st,
                      workspace, grid, 3 * C, dgamma, dbeta, dabias, C);
   HVK_CHECK_LAUNCH("ln_bwd_colsum");

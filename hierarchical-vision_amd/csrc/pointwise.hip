@@ -41,9 +41,13 @@ __global__ __launch_bounds__(64 * kWaves) void bias_gelu_bwd_kernel(const hvk_bf
                                                                     const hvk_bf16* __restrict__ gy,
                                                                     hvk_bf16* __restrict__ gh,
                                                                     float* __restrict__ part,
+                                                                    float* __restrict__ dbias,
                                                                     int rows, int N) {
   __shared__ float red[kWaves][512];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // dbias is accumulated by the colsum kernel that follows in the stream: zero it here
+  if (dbias && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) dbias[i] = 0.f;
   const int c = (blockIdx.y * 64 + lane) * 8;
   const bool act = c < N;
   float bb[8], acc[8];
@@ -128,11 +132,9 @@ int hvk_bias_gelu_bwd(const void* h, const float* bias, const void* gy, void* gh
   dim3 grid(gx, (N + 511) / 512);
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, grid, dim3(64 * kWaves), 0, st,
                      static_cast<const hvk_bf16*>(h), bias, static_cast<const hvk_bf16*>(gy),
-                     static_cast<hvk_bf16*>(gh), workspace, rows, N);
+                     static_cast<hvk_bf16*>(gh), workspace, dbias, rows, N);
   HVK_CHECK_LAUNCH("bias_gelu_bwd");
   if (dbias) {
-    if (hipMemsetAsync(dbias, 0, sizeof(float) * N, st) != hipSuccess)
-      return hvk_set_error(HVK_EHIP, "hvk_bias_gelu_bwd: memset failed");
     hipLaunchKernelGGL(colsum_rows_kernel, dim3((N + 63) / 64, 16), dim3(64), 0, st, workspace,
                        gx, N, dbias);
     HVK_CHECK_LAUNCH("bias_gelu_colsum");

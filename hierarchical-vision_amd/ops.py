@@ -189,6 +189,54 @@ def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift
                                      shift)
 
 
+# --------------------------------------------------------------------------- CPB table
+_CPB_WS = {}
+
+
+class CpbTable(torch.autograd.Function):
+    """(table [nH, RR], scale [nH]) = (16 sigmoid(cpb_mlp(coords)) transposed, exp(clamp(
+    logit_scale))) in one launch (hvk_cpb_fwd); backward two launches (hvk_cpb_bwd).
+    Replaces swinv2.py:230 and 233-246 (before the rpi gather)."""
+
+    @staticmethod
+    def forward(ctx, coords, w1, b1, w2, logit_scale, clamp_max):
+        coords, w1, b1, w2 = _f32(coords), _f32(w1), _f32(b1), _f32(w2)
+        logit = _f32(logit_scale.reshape(-1))
+        nH, hid = w2.shape
+        RR = coords.shape[0]
+        table = torch.empty((nH, RR), device=w1.device, dtype=torch.float32)
+        scale = torch.empty(nH, device=w1.device, dtype=torch.float32)
+        call("hvk_cpb_fwd", ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), float(clamp_max),
+             RR, nH, hid, ptr(table), ptr(scale), stream())
+        ctx.save_for_backward(coords, w1, b1, w2, logit, table)
+        ctx.clamp_max = float(clamp_max)
+        ctx.logit_shape = logit_scale.shape
+        return table, scale
+
+    @staticmethod
+    def backward(ctx, dtable, dscale):
+        coords, w1, b1, w2, logit, table = ctx.saved_tensors
+        nH, hid = w2.shape
+        RR = coords.shape[0]
+        dtable = _f32(dtable) if dtable is not None else torch.zeros_like(table)
+        dscale = _f32(dscale) if dscale is not None else torch.zeros_like(logit)
+        dw1, db1, dw2 = torch.empty_like(w1), torch.empty_like(b1), torch.empty_like(w2)
+        dlogit = torch.empty_like(logit)
+        nbytes = _lib.load().hvk_cpb_bwd_workspace_bytes(RR, nH)
+        key = (w1.device, nbytes)
+        ws = _CPB_WS.get(key)
+        if ws is None:
+            ws = _CPB_WS[key] = torch.empty(nbytes // 4, device=w1.device, dtype=torch.float32)
+        call("hvk_cpb_bwd", ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), ctx.clamp_max, RR,
+             nH, hid, ptr(table), ptr(dtable), ptr(dscale), ptr(dw1), ptr(db1), ptr(dw2),
+             ptr(dlogit), ptr(ws), nbytes, stream())
+        return None, dw1, db1, dw2, dlogit.reshape(ctx.logit_shape), None
+
+
+def cpb_table(coords, w1, b1, w2, logit_scale, clamp_max):
+    return CpbTable.apply(coords, w1, b1, w2, logit_scale, clamp_max)
+
+
 # --------------------------------------------------------------------------- LayerNorm
 class LayerNormResidual(torch.autograd.Function):
     """x = x0 + s[b] * LayerNorm(a + abias); returns (x f32, x bf16 copy).  abias is the

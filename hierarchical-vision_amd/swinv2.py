@@ -165,12 +165,22 @@ class WindowAttention(nn.Module):
         self.input_resolution = None
         self.shift_size = 0
 
-    # small per-block tables, computed in f32 outside autocast (the kernel consumes them)
-    def bias_table(self):
-        """16*sigmoid(cpb_mlp(relative_coords_table)) as [nH, (2w-1)^2] f32."""
+    # small per-block tables (f32, one fused launch: ops.cpb_table / csrc/cpb.hip)
+    def cpb_tables(self):
+        """(16*sigmoid(cpb_mlp(relative_coords_table)) as [nH, (2w-1)^2] f32,
+        exp(clamp(logit_scale, max=ln 100)) as [nH] f32) (swinv2.py:230, 233-246)."""
+        l1, l2 = self.cpb_mlp[0], self.cpb_mlp[2]
+        if (isinstance(self.cpb_mlp[1], nn.ReLU) and l1.bias is not None and l2.bias is None
+                and l1.out_features == 512 and self.num_heads <= 32):
+            return ops.cpb_table(self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias,
+                                 l2.weight, self.logit_scale, float(self.logit_clamp_max))
         with torch.autocast(device_type=self.logit_scale.device.type, enabled=False):
             t = self.cpb_mlp(self.relative_coords_table.reshape(-1, 2).float())
-            return (16 * torch.sigmoid(t)).t().contiguous()
+            return (16 * torch.sigmoid(t)).t().contiguous(), self.scales()
+
+    def bias_table(self):
+        """16*sigmoid(cpb_mlp(relative_coords_table)) as [nH, (2w-1)^2] f32."""
+        return self.cpb_tables()[0]
 
     def scales(self):
         """exp(clamp(logit_scale, max=ln 100)) as [nH] f32 (swinv2.py:230)."""
@@ -198,7 +208,8 @@ class WindowAttention(nn.Module):
         proj's bias when proj_bias=False: the caller folds self.proj_bias() into the next
         kernel)."""
         qkv = ops.linear(x, self.qkv.weight, self.qkv_gemm_bias())
-        o = ops.window_attention_core(qkv, self.bias_table(), self.scales(), H, W, self.num_heads,
+        table, scale = self.cpb_tables()
+        o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
                                       self.window_size[0], shift, q_bias=self.q_bias)
         return self.proj_drop(ops.linear(o, self.proj.weight, self.proj_bias() if proj_bias else None))
 

@@ -82,6 +82,24 @@ int hvk_linear_gelu_supported(int M, int K, int N);
 int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                         int K, int N, void* stream);
 
+/* ---- Continuous relative-position bias table + logit scale (one block) ---------------
+ * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
+ * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,
+ * before the rpi gather) and 230 (clamp + exp).  coords: f32 [RR, 2]
+ * (relative_coords_table), w1 f32 [512, 2], b1 [512], w2 [nH, 512], logit_scale [nH];
+ * table f32 [nH, RR], scale [nH].  hidden must be 512, nH <= 32.  Backward: from the
+ * forward table and d table / d scale, writes dw1, db1, dw2, d logit_scale (all
+ * overwritten) using hvk_cpb_bwd_workspace_bytes of workspace. */
+int hvk_cpb_fwd(const float* coords, const float* w1, const float* b1, const float* w2,
+                const float* logit_scale, float clamp_max, int RR, int nH, int hidden,
+                float* table, float* scale, void* stream);
+size_t hvk_cpb_bwd_workspace_bytes(int RR, int nH);
+int hvk_cpb_bwd(const float* coords, const float* w1, const float* b1, const float* w2,
+                const float* logit_scale, float clamp_max, int RR, int nH, int hidden,
+                const float* table, const float* dtable, const float* dscale, float* dw1,
+                float* db1, float* dw2, float* dlogit, float* workspace, size_t workspace_bytes,
+                void* stream);
+
 /* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
  * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)
  * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(proj(x))) with proj/fc2 run
