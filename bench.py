@@ -40,6 +40,11 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: time HIP-graph replays of the step (trainer.capture/replay); 0: eager "
+                         "(default: keeps the RCCL all-reduce overlapped with the backward)")
+    ap.add_argument("--roofline-steps", type=int, default=4,
+                    help="graph mode: eager warm-up steps whose W-MSA launches are timed")
     return ap.parse_args()
 
 
@@ -151,23 +156,43 @@ def main():
     img = model.module.patch_embed.img_size[0]
     batch = synthetic_batch(args, tax, rank, device, img)
 
-    for _ in range(args.warmup):
-        trainer.train_step(batch)
     fwd_bytes, bwd_bytes = wmsa_algorithmic_bytes(model.module, args.batch)
     timing = not args.no_roofline
+    timer, timed_steps = None, args.steps
+    if args.graph:
+        # eager warm-up; the last roofline_steps of it carry the W-MSA kernel timer (graph
+        # replays cannot: per-kernel dispatch events are not captured), then capture
+        rsteps = min(args.roofline_steps, max(args.warmup, 1)) if timing else 0
+        for i in range(max(args.warmup, 1)):
+            if timing and i == max(args.warmup, 1) - rsteps:
+                torch.cuda.synchronize()
+                ops.kernel_timer_start()
+            trainer.train_step(batch)
+        if timing:
+            torch.cuda.synchronize()
+            timer, timed_steps = ops.kernel_timer_stop(), rsteps
+        trainer.capture(batch)
+        step = trainer.replay
+    else:
+        for _ in range(args.warmup):
+            trainer.train_step(batch)
+
+        def step():
+            return trainer.train_step(batch)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if timing:  # W-MSA launches timed by their own dispatch packets (libhvk kernel timer)
+    if timing and not args.graph:  # W-MSA launches timed by their own dispatch packets
         ops.kernel_timer_start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = trainer.train_step(batch)
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timer = ops.kernel_timer_stop() if timing else None
+    if timing and not args.graph:
+        timer = ops.kernel_timer_stop()
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -187,30 +212,34 @@ def main():
         "config": {"workload": "SwinV2-T 224 w7 + HXE (10000 leaves, 7 tiers) train step",
                    "model": args.model, "loss": args.loss, "global_batch": world * args.batch,
                    "per_gpu_batch": args.batch, "image_size": img,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "execution": "hip-graph replay" if args.graph else "eager"},
         "value_per_gpu": round(value / world, 2),
         "final_loss": round(loss_val, 4),
     }
     if timer:
         fw_ms, fw_n = timer["wmsa_fwd"]
         bw_ms, bw_n = timer["wmsa_bwd"]
-        n_launch = fw_n // args.steps
-        fwd_gbs = fwd_bytes * args.steps / (fw_ms / 1000) / 1e9
-        bwd_gbs = bwd_bytes * args.steps / (bw_ms / 1000) / 1e9
+        n_launch = fw_n // timed_steps
+        fwd_gbs = fwd_bytes * timed_steps / (fw_ms / 1000) / 1e9
+        bwd_gbs = bwd_bytes * timed_steps / (bw_ms / 1000) / 1e9
         result["roofline"] = {
             "kernel": "wmsa_fwd_kernel<7> (all %d launches per step)" % n_launch,
             "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "algorithmic_bytes_per_step": fwd_bytes,
             "avg_launch_us": round(1000 * fw_ms / fw_n, 2),
-            "ms_per_step": round(fw_ms / args.steps, 3),
-            "timing": "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps"}
+            "ms_per_step": round(fw_ms / timed_steps, 3),
+            "timing": ("dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps just "
+                       "before the graph capture (replays carry no per-kernel events)" % timed_steps
+                       if args.graph else
+                       "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps")}
         result["roofline_bwd"] = {
             "kernel": "wmsa_bwd_kernel<7>", "bound": "hbm", "achieved": round(bwd_gbs, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
             "algorithmic_bytes_per_step": bwd_bytes,
             "avg_launch_us": round(1000 * bw_ms / bw_n, 2),
-            "ms_per_step": round(bw_ms / args.steps, 3)}
+            "ms_per_step": round(bw_ms / timed_steps, 3)}
     if rank == 0 and world == 1 and args.cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:

@@ -27,6 +27,7 @@ class GradientBuckets:
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
         self.enabled = self.world > 1
+        self.defer = False  # graph mode: no hook-launched all-reduce (allreduce_now() instead)
         self.buckets = []
         self._hooks = []
         if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
@@ -64,7 +65,7 @@ class GradientBuckets:
     def _make_hook(self, bi):
         def hook(p):
             self._pending[bi] -= 1
-            if self._pending[bi] == 0 and self.enabled:
+            if self._pending[bi] == 0 and self.enabled and not self.defer:
                 flat = self.buckets[bi][0]
                 self._works[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg,
                                                   async_op=True)
@@ -95,6 +96,23 @@ class GradientBuckets:
             if w is None:  # a bucket whose grads never arrived (unused params): reduce now
                 w = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             w.wait()
+            flat.div_(self.world)
+
+    def zero_(self):
+        """Zero the buckets in place (graph mode: captured at the start of the backward graph)."""
+        for flat, _ in self.buckets:
+            flat.zero_()
+
+    def allreduce_now(self):
+        """Graph mode: all-reduce every bucket (SUM) between the backward and optimizer graph
+        replays, eagerly (RCCL is not captured); the mean is taken inside the optimizer graph."""
+        works = [dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                 for flat, _ in self.buckets]
+        for w in works:
+            w.wait()
+
+    def scale_(self):
+        for flat, _ in self.buckets:
             flat.div_(self.world)
 
     def flat_buffers(self):

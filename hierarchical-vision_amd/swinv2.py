@@ -143,6 +143,7 @@ class WindowAttention(nn.Module):
             raise NotImplementedError("square windows only")
         self.logit_scale = nn.Parameter(torch.log(10 * torch.ones((num_heads, 1, 1))))
         self.register_buffer("logit_clamp_max", torch.log(torch.tensor(1.0 / 0.01)))
+        self._logit_clamp = float(self.logit_clamp_max)  # host copy: no device sync per step
         self.cpb_mlp = nn.Sequential(nn.Linear(2, 512, bias=True), nn.ReLU(inplace=True),
                                      nn.Linear(512, num_heads, bias=False))
         self.register_buffer("relative_coords_table",
@@ -173,7 +174,7 @@ class WindowAttention(nn.Module):
         if (isinstance(self.cpb_mlp[1], nn.ReLU) and l1.bias is not None and l2.bias is None
                 and l1.out_features == 512 and self.num_heads <= 32):
             return ops.cpb_table(self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias,
-                                 l2.weight, self.logit_scale, float(self.logit_clamp_max))
+                                 l2.weight, self.logit_scale, self._logit_clamp)
         with torch.autocast(device_type=self.logit_scale.device.type, enabled=False):
             t = self.cpb_mlp(self.relative_coords_table.reshape(-1, 2).float())
             return (16 * torch.sigmoid(t)).t().contiguous(), self.scales()

@@ -1,0 +1,50 @@
+"""Graph-mode training (Trainer.capture / replay: the step as two HIP graphs) gives the same
+parameters as eager steps from the same start (drop-path off: no RNG in the step)."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed=0):
+    from hvamd import hierarchy, models, optim, swinv2
+    from hvamd.algorithmic import GradientClipping
+    from hvamd.trainer import Trainer
+    torch.manual_seed(seed)
+    dev = torch.device("cuda:0")
+    tax = hierarchy.Taxonomy.synthetic((2, 3, 4, 5, 6, 7, 12))
+    net = swinv2.SwinTransformerV2(img_size=56, embed_dim=32, depths=[2, 2], num_heads=[1, 2],
+                                   window_size=7, num_classes=tax.num_leaves,
+                                   drop_path_rate=0.0).to(dev)
+    loss_fn = hierarchy.HierarchicalCrossEntropy(tax, tree_weights="exponential").to(dev)
+    model = models.Model(net, None, None, loss_fn)
+    return tax, model, dev
+
+
+def _trainer(model):
+    from hvamd import optim
+    from hvamd.algorithmic import GradientClipping
+    from hvamd.trainer import Trainer
+    opt = optim.DecoupledSGDW(optim.set_weight_decay(model), lr=0.05, momentum=0.9,
+                              weight_decay=5e-4)
+    return Trainer(model, opt, [GradientClipping("norm", 2.0)])
+
+
+def test_graph_replay_matches_eager():
+    tax, model, dev = _setup()
+    model_b = copy.deepcopy(model)
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(4, 3, 56, 56, device=dev, generator=g)
+    y = torch.tensor(tax.leaf_paths[[1, 5, 9, 11]], device=dev)
+    ta, tb = _trainer(model), _trainer(model_b)
+    la = [ta.train_step((x, y)) for _ in range(6)]
+    tb.capture((x, y), warmup=3)      # 3 eager steps inside, then capture
+    lb = [tb.replay().clone() for _ in range(3)]
+    torch.cuda.synchronize()
+    for a, b in zip(la[3:], lb):
+        assert abs(a.item() - b.item()) < 1e-3 * max(1.0, abs(a.item())), (a.item(), b.item())
+    for (na, pa), (nb, pb) in zip(model.named_parameters(), model_b.named_parameters()):
+        rel = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-3, (na, rel)
