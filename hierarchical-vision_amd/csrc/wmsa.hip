@@ -640,23 +640,27 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
   a.out = static_cast<hvk_bf16*>(out);
   a.bias = bias_table;
   a.scale = scale;
-  // resident workgroups: 256 CUs x 4 (<=128 VGPRs -> 4 waves/SIMD); HVK_WMSA_FWD_WGS overrides
-  static const int cap = [] {
-    const char* e = getenv("HVK_WMSA_FWD_WGS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 256 * 4;
-  }();
-  int rc = make_geom(B, H, W, C, num_heads, window, shift, cap, a.g);
-  if (rc) return rc;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hvk_wmsa::large_window(window)) return hvk_wmsa::large_fwd(a, window, st);
+  if (hvk_wmsa::large_window(window)) {
+    int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);
+    if (rc) return rc;
+    return hvk_wmsa::large_fwd(a, window, st);
+  }
+  if (window != 4 && window != 6 && window != 7 && window != 8)
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8,12,16,24)", window);
+  // HVK_WMSA_FWD_V1=1: the round-1 wave-per-(window, head) kernel (A/B timing only)
+  static const bool v1 = [] {
+    const char* e = getenv("HVK_WMSA_FWD_V1");
+    return e && atoi(e) > 0;
+  }();
+  if (!v1) return hvk_wmsa::ring_fwd(a, B, H, W, C, num_heads, window, shift, st);
+  int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);
+  if (rc) return rc;
   switch (window) {
     case 7: return launch_fwd<7>(a, st);
     case 8: return launch_fwd<8>(a, st);
     case 6: return launch_fwd<6>(a, st);
-    case 4: return launch_fwd<4>(a, st);
-    default:
-      return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8,12,16,24)", window);
+    default: return launch_fwd<4>(a, st);
   }
 }
 

@@ -102,6 +102,10 @@ size_t large_acc_floats(int num_heads, int win);  // dbias_acc floats (bins)
 int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,
               hipStream_t st);
 
+// windows <= 8, forward (wmsa_ring.hip): one persistent workgroup per (window chunk, head
+// group), window slabs staged by LDS-DMA
+int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);
+
 // finalize helper: per head block, write dscale / dq_bias from the workspace and zero it
 __device__ __forceinline__ void finalize_scale_qb(float* dscale_acc, float* dqb_acc, float* dscale,
                                                   float* dqb, int h) {

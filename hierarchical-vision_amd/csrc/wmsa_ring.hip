@@ -1,0 +1,492 @@
+// W-MSA forward for windows <= 8 on gfx950: persistent workgroups that stream window slabs
+// through LDS by LDS-DMA.  Same math as the reference sequence listed in wmsa.hip
+// (swinv2.py:221-261 with the roll/partition/reverse of 399-429 folded into addressing).
+//
+// Work unit: (window, group of HG heads); a workgroup = HG waves (one per head) walks a
+// contiguous chunk of windows for one head group.  Per window:
+//   1. the window's q/k/v bytes of the head group are staged into one LDS "slab"
+//      [N tokens][3 parts][HG*32] bf16 (RS = 12*HG 16-B slots per token) by
+//      global_load_lds_dwordx4, filled lane-linearly (slot = 64*instr + lane): every DMA
+//      wave-instruction reads whole row segments (HG*64 B per token and part; at HG = nH the
+//      full 6C-byte row, and the 7 tokens of a window row are adjacent in memory);
+//   2. each wave copies its head's q/k fragments (ds_read_b128) and V^T fragments
+//      (ds_read_b64_tr_b16) into registers, the workgroup syncs, and the NEXT window's DMA is
+//      issued into the same slab, so it is in flight during this window's math and stores;
+//   3. S^T = K^ (scale log2e Q^)^T + bias on MFMA with the CPB bias as the C operand,
+//      gathered from a compact per-head LDS table by ds_read_b32 with compile-time offsets;
+//      softmax in registers; O^T = V^T P^T on MFMA; 16-B output stores per lane.
+// Tokens of a window sit in the 16-row MFMA tiles on a PW-wide grid (PW = 8; 4 for w4):
+// position p = PW*y + x.  The rel-pos index of (query p, key p') is then
+// TR*(qi - ki) - r + base(lane) with TR = (16/PW)(2w-1): one lane-constant VGPR plus an
+// immediate offset per (qi, ki, r), no address arithmetic in the loop.  Grid positions with
+// x >= w or y >= w are padding: zero fragments, zero V rows, -inf scores.
+#include <stdlib.h>
+
+#include "wmsa_common.h"
+
+#ifndef HVK_RING_PROBE
+#define HVK_RING_PROBE 0
+#endif
+
+namespace {
+using namespace hvk_wmsa;
+
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* gbl_vptr;
+
+constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
+
+template <int WIN, int HG>
+struct RingCfg {
+  static constexpr int PW = WIN <= 4 ? 4 : 8;        // grid width of a window in the tiles
+  static constexpr int N = WIN * WIN;                // real tokens
+  static constexpr int NT = (WIN * PW + 15) / 16;    // 16-row tiles
+  static constexpr int NC = (NT + 1) / 2;            // 32-key chunks (one MFMA K-step)
+  static constexpr int R = 2 * WIN - 1;
+  static constexpr int TR = (16 / PW) * R;           // index step per tile
+  static constexpr int RS = 12 * HG;                 // 16-B slots per token in the slab
+  // the slab is WIN runs (window rows) of IPR DMA instructions: a run holds the WIN tokens of
+  // one window row (adjacent in memory), so a lane's (token column, part, 16-B column) is the
+  // same for instruction m of every run, of every window
+  static constexpr int IPR = (WIN * RS + 63) / 64;   // DMA wave-instructions per run
+  static constexpr int RUN = IPR * 64;               // slots per run
+  static constexpr int NINST = WIN * IPR;            // DMA wave-instructions per slab
+  static constexpr int SLAB = NINST * 1024;
+  static constexpr int NK = (NINST + HG - 1) / HG;   // DMA instructions per wave
+  static constexpr int KP = IPR / gcd(HG, IPR);      // period of instruction m over a wave's k
+  // compact bias table per head: R*R entries (x log2e) inside zero padding that absorbs the
+  // (never used) indices of padded grid positions
+  static constexpr int LQMAX = PW == 8 ? R + 7 : 3 * R + 3;
+  static constexpr int LKMAX = PW == 8 ? R + 4 : 3 * R;
+  static constexpr int BASE0 = (WIN - 1) * (R + 1);
+  static constexpr int LO = BASE0 - LKMAX - TR * (NT - 1) - 3;   // smallest index read
+  static constexpr int PAD = LO < 0 ? -LO : 0;
+  static constexpr int HI = BASE0 + LQMAX + TR * (NT - 1);       // largest index read
+  static constexpr int TABF = ((PAD + (HI + 1 > R * R ? HI + 1 : R * R) + 3) / 4) * 4;
+  static constexpr int LDS = SLAB + 16 + HG * TABF * 4;
+  static_assert(NT <= 4, "window larger than 8 needs the large-window kernels");
+};
+
+// LDS byte address of a pointer into dynamic shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+// LDS reads issued from inline asm: the compiler's waitcnt pass does not see them, so it
+// cannot add the conservative vmcnt(0) it inserts before LDS reads while an LDS-DMA may be
+// pending (that would also wait for this workgroup's outstanding output stores).  The caller
+// waits lgkmcnt(0) and then ties the results (lds_fence).
+template <int OFF>
+__device__ __forceinline__ hvk_u32x4 lds_rd128(uint32_t a) {
+  hvk_u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int OFF>
+__device__ __forceinline__ hvk_u32x2 lds_rd64_tr(uint32_t a) {
+  hvk_u32x2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+template <int O0, int O1>
+__device__ __forceinline__ hvk_u32x2 lds_rd2(uint32_t a) {
+  hvk_u32x2 r;
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(r) : "v"(a), "i"(O0), "i"(O1));
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void lds_fence(T& v) {
+  asm volatile("" : "+v"(v));
+}
+__device__ __forceinline__ uint4 u4(hvk_u32x4 v) { return make_uint4(v[0], v[1], v[2], v[3]); }
+
+// output row segment store: plain (default) or nontemporal (HVK_RING_NT_STORE, A/B builds)
+__device__ __forceinline__ void ring_store(hvk_bf16* dst, uint4 v) {
+#ifdef HVK_RING_NT_STORE
+  __builtin_nontemporal_store(__builtin_bit_cast(hvk_u32x4, v), reinterpret_cast<hvk_u32x4*>(dst));
+#else
+  *reinterpret_cast<uint4*>(dst) = v;
+#endif
+}
+
+// the 2*NT ds_read2_b32 of one query tile's bias C operands (compile-time offsets)
+template <int TR, int NT, int QI, int KI = 0>
+__device__ __forceinline__ void ring_bias_read(hvk_u32x2 (&br)[NT][2], uint32_t a) {
+  if constexpr (KI < NT) {
+    constexpr int off = TR * (NT - 1 - QI + KI);
+    br[KI][0] = lds_rd2<off, off + 1>(a);
+    br[KI][1] = lds_rd2<off + 2, off + 3>(a);
+    ring_bias_read<TR, NT, QI, KI + 1>(br, a);
+  }
+}
+template <int TR, int NT>
+__device__ __forceinline__ void ring_bias_read_q(hvk_u32x2 (&br)[NT][2], uint32_t a, int qi) {
+  if constexpr (NT > 0) if (qi == 0) ring_bias_read<TR, NT, 0>(br, a);
+  if constexpr (NT > 1) if (qi == 1) ring_bias_read<TR, NT, (NT > 1 ? 1 : 0)>(br, a);
+  if constexpr (NT > 2) if (qi == 2) ring_bias_read<TR, NT, (NT > 2 ? 2 : 0)>(br, a);
+  if constexpr (NT > 3) if (qi == 3) ring_bias_read<TR, NT, (NT > 3 ? 3 : 0)>(br, a);
+}
+
+// padded-grid position -> window token (-1 for padding)
+template <int WIN, int PW>
+__device__ __forceinline__ int grid_token(int p) {
+  const int y = p / PW, x = p % PW;
+  return (x < WIN && y < WIN) ? y * WIN + x : -1;
+}
+
+template <int WIN, int HG>
+__global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
+  using K = RingCfg<WIN, HG>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WmsaGeom& g = a.g;
+  const int ng = g.nH / HG;
+  const int bid = blockIdx.x, xcd = bid & 7, loc = bid >> 3;
+  const int grp = loc % ng, chunk = (loc / ng) * 8 + xcd;  // a chunk's groups share an XCD
+  if (chunk >= g.n_chunks) return;
+  const int w0 = (int)((long long)chunk * g.n_windows / g.n_chunks);
+  const int w1 = (int)((long long)(chunk + 1) * g.n_windows / g.n_chunks);
+  if (w0 >= w1) return;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int li = lane & 15, gq = lane >> 4;
+  const int C = g.C;
+  const int h = grp * HG + wave;
+  const int per_img = g.nWh * g.nWw;
+  const char* qkv = reinterpret_cast<const char*>(a.qkv);
+  const size_t row_bytes = (size_t)6 * C;
+  const int grp_off = grp * HG * 64;  // byte offset of the group inside a q/k/v part
+
+  char* zero16 = smem + K::SLAB;
+  float* btab = reinterpret_cast<float*>(smem + K::SLAB + 16);
+
+  // LDS-DMA of a window's slab.  Slot P = RUN*ty + 64m + lane of instruction j = IPR*ty + m
+  // holds token (ty, tx), part, 16-B column c with (tx, part, c) fixed by (m, lane): each lane
+  // keeps pre[k % KP] = tx*RB + part*2C + 16c + group offset (bits 0-23) | tx << 24 for its
+  // k-th instruction (j = wave + HG*k) and the window adds one uniform row offset.  Slots past
+  // a run's WIN*RS are never read: they load the run's first bytes again (no exec masking).
+  // Offsets are 32-bit from the image base; a window's rows wrap around the image (cyclic
+  // shift) only on the last window row (uniform test) / column (per lane, edge windows only).
+  const unsigned RB = 6u * C, WRB = (unsigned)g.W * RB, HWRB = (unsigned)g.H * WRB;
+  unsigned pre[K::KP];
+#pragma unroll
+  for (int k = 0; k < K::KP; ++k) {
+    const int m = (wave + HG * k) % K::IPR;
+    const unsigned q = 64u * m + lane;
+    unsigned v = grp_off;
+    if (q < (unsigned)(WIN * K::RS)) {
+      const unsigned tx = q / K::RS, r = q - tx * K::RS;
+      const unsigned part = r / (4 * HG), c = r - part * (4 * HG);
+      v = (tx * RB + part * 2 * C + c * 16 + grp_off) | (tx << 24);
+    }
+    pre[k] = v;
+  }
+  auto issue = [&](int b, int wh, int ww) {
+    const char* img = qkv + (size_t)b * HWRB;
+    const int y0 = wh * WIN + g.shift, x0 = ww * WIN + g.shift;
+    const int ly = g.H - y0, lx = g.W - x0;  // ty >= ly (tx >= lx): the row wraps
+#pragma unroll
+    for (int k = 0; k < K::NK; ++k) {
+      const int j = wave + HG * k;
+      if (j < K::NINST) {
+        const int ty = j / K::IPR;
+        const unsigned U = ((unsigned)(y0 + ty - (ty >= ly ? g.H : 0)) * g.W + x0) * RB;  // uniform
+        unsigned off = __umul24(pre[k % K::KP], 1u) + U;  // v_mad_u32_u24: low 24 bits of pre
+        if (lx < WIN)  // last window column: per-lane wrap of the token column
+          off -= ((int)(pre[k % K::KP] >> 24) >= lx) ? WRB : 0u;
+        __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0,
+                                         2 /* nontemporal: every byte is read once */);
+      }
+    }
+  };
+  // per-workgroup setup, overlapping nothing yet: bias tables = bias*log2e - M_h, where
+  // M_h = scale*log2e + max(bias)*log2e bounds every logit of head h from above.  Softmax is
+  // shift invariant, so exp2 of the shifted logits needs no row max: each query's own key has
+  // cos = 1, so its shifted logit is >= -16*log2e and the row sum cannot underflow.
+  // stored mirrored (entry PAD + i at TABF - 1 - PAD - i): the 4 accumulator rows r of a
+  // (query tile, key tile) pair are then 4 ASCENDING dwords, read by two ds_read2_b32 straight
+  // into the MFMA C operand
+  for (int e = threadIdx.x; e < HG * K::TABF; e += 64 * HG) {
+    const int hl = e / K::TABF, i = K::TABF - 1 - e % K::TABF - K::PAD;
+    btab[e] = (i >= 0 && i < K::R * K::R) ? a.bias[(size_t)(grp * HG + hl) * K::R * K::R + i] * HVK_LOG2E
+                                          : 0.f;
+  }
+  if (threadIdx.x == 0) *reinterpret_cast<uint4*>(zero16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  {
+    float mb = -INFINITY;
+    float* tb = btab + wave * K::TABF + K::TABF - K::PAD - K::R * K::R;  // mirrored real entries
+    for (int i = lane; i < K::R * K::R; i += 64) mb = fmaxf(mb, tb[i]);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
+    const float Mh = a.scale[h] * HVK_LOG2E + mb;
+    for (int i = lane; i < K::R * K::R; i += 64) tb[i] -= Mh;
+  }
+  const float sc2 = a.scale[h] * HVK_LOG2E;
+  const float mask2 = -100.f * HVK_LOG2E;
+  // lane constants: bias base index, key-slot coordinates (slot bit ki*4 + r)
+  int lq, lk;
+  if (K::PW == 8) {
+    lq = (li >> 3) * K::R + (li & 7);
+    lk = (gq >> 1) * K::R + 4 * (gq & 1);
+  } else {
+    lq = (li >> 2) * K::R + (li & 3);
+    lk = gq * K::R;
+  }
+  // bias(query tile qi, key tile ki, row r) sits at dword TR*(NT - 1 - qi + ki) + r from bta:
+  // non-negative immediates < 256 (the ds_read2_b32 offset fields)
+  const uint32_t bta =
+      lds_addr(btab) + 4 * (wave * K::TABF + K::TABF - 4 - (K::PAD + K::BASE0 + lq - lk - K::TR * (K::NT - 1) - 3) -
+                            2 * K::TR * (K::NT - 1));
+  static_assert(2 * K::TR * (K::NT - 1) + 3 < 256, "bias offsets exceed ds_read2_b32's field");
+  // A operand of the row-sum MFMA: 1.0 for real keys of chunk c in k-slot order (B operand
+  // of P^T: slot 8gq + j <-> key 32c + 4gq + j, j < 4; 32c + 16 + 4gq + j - 4, j >= 4)
+  uint4 ones[K::NC];
+#pragma unroll
+  for (int c = 0; c < K::NC; ++c) {
+    uint32_t wv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * jj + e;
+        const int p = 32 * c + (j < 4 ? 4 * gq + j : 16 + 4 * gq + j - 4);
+        if ((p % K::PW) < WIN && (p / K::PW) < WIN) v |= 0x3F80u << (16 * e);
+      }
+      wv[jj] = v;
+    }
+    ones[c] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+  // key-slot region bits (slot bit ki*4 + r): row band in bits 0-15, column band in 16-31
+  uint32_t kband = 0;
+#pragma unroll
+  for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 16 * ki + 4 * gq + r, ky = p / K::PW, kx = p % K::PW;
+      if (ky >= WIN - g.shift) kband |= 1u << (ki * 4 + r);
+      if (kx >= WIN - g.shift) kband |= 1u << (16 + ki * 4 + r);
+    }
+  const int hs = wave * 4 + gq;  // this lane's 16-B slot inside a part of a token
+
+  // window coordinates advance incrementally (no per-window integer divisions)
+  int cb = w0 / per_img, cwh = (w0 % per_img) / g.nWw, cww = w0 % g.nWw;
+  issue(cb, cwh, cww);
+  const uint32_t zaddr = lds_addr(zero16);
+  for (int w = w0; w < w1; ++w) {
+    // this window's slab has landed: at w > w0 the NT output stores of the previous window
+    // were issued after its DMA and may still be in flight
+    if (w == w0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::NT) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // lane coordinates recomputed per window (kept out of the loop-invariant pool: VGPRs)
+    int l16 = li, g4 = gq;
+    asm volatile("" : "+v"(l16), "+v"(g4));
+    hvk_u32x4 qr[K::NT], kr[K::NT];
+    hvk_u32x2 vr[K::NC][2][2];
+    {
+      // tile i, lane li: grid (y, x) = ((16/PW) i + li/PW, li%PW): token = (16/PW) WIN i + base
+      const int x = l16 % K::PW, y0 = l16 / K::PW;
+      const uint32_t fb = lds_addr(smem) + (y0 * K::RUN + x * K::RS + wave * 4 + g4) * 16;
+#pragma unroll
+      for (int i = 0; i < K::NT; ++i) {
+        const bool ok = x < WIN && y0 + (16 / K::PW) * i < WIN;
+        const uint32_t aq = fb + (16 / K::PW) * i * K::RUN * 16;
+        qr[i] = lds_rd128<0>(ok ? aq : zaddr);
+        kr[i] = lds_rd128<0>(ok ? aq + 4 * HG * 16 : zaddr);
+      }
+    }
+    {
+      // V^T fragments: chunk c, lane (li, gq), dt: key position p = 32c + 16h + 4gq + li/4
+      // (h = 0, 1 for the two 8-B halves), channels d = 8(li&3) + 4dt ..+3; the output
+      // accumulator o[dt][r] of lane (q, gq) then holds d = 8gq + 4dt + r (8 consecutive
+      // channels per lane: one 16-B store).  Padding keys read 16 zero bytes.
+      const int pl = 4 * g4 + (l16 >> 2);  // p - 32c - 16h, in [0, 16)
+      const int x = pl % K::PW, y0 = pl / K::PW;
+      const uint32_t vb = lds_addr(smem) + (y0 * K::RUN + x * K::RS) * 16 +
+                          (2 * HG * 32 + wave * 32 + 8 * (l16 & 3)) * 2;
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int dy = (16 / K::PW) * (2 * c + hh);
+          const bool ok = x < WIN && y0 + dy < WIN;
+          const uint32_t av = ok ? vb + dy * K::RUN * 16 : zaddr;
+          vr[c][0][hh] = lds_rd64_tr<0>(av);
+          vr[c][1][hh] = lds_rd64_tr<8>(av);  // zero16 + 8 is zero as well
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint4 qf[K::NT], kf[K::NT], vt[K::NC][2];
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      lds_fence(qr[i]);
+      lds_fence(kr[i]);
+      qf[i] = u4(qr[i]);
+      kf[i] = u4(kr[i]);
+    }
+#pragma unroll
+    for (int c = 0; c < K::NC; ++c)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        lds_fence(vr[c][dt][0]);
+        lds_fence(vr[c][dt][1]);
+        vt[c][dt] = make_uint4(vr[c][dt][0][0], vr[c][dt][0][1], vr[c][dt][1][0], vr[c][dt][1][1]);
+      }
+    __builtin_amdgcn_s_barrier();  // every wave holds its fragments: the slab is free
+    asm volatile("" ::: "memory");
+    int nb = cb, nwh = cwh, nww = cww + 1;
+    if (nww == g.nWw) {
+      nww = 0;
+      if (++nwh == g.nWh) {
+        nwh = 0;
+        ++nb;
+      }
+    }
+#if HVK_RING_PROBE == 2  // tools/probe: math only (the first slab is reused, no DMA)
+    (void)nb;
+#else
+    if (w + 1 < w1) issue(nb, nwh, nww);
+#endif
+
+    const int b = cb, wh = cwh, ww = cww;
+    cb = nb;
+    cwh = nwh;
+    cww = nww;
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+#if HVK_RING_PROBE == 1  // tools/probe: memory only (same DMA and stores, no math)
+#pragma unroll
+    for (int qi = 0; qi < K::NT; ++qi) {
+      const int tq = grid_token<WIN, K::PW>(16 * qi + li);
+      if (tq >= 0) {
+        uint4 v = qf[qi];
+        v.x ^= kf[qi].x ^ vt[0][0].x;
+        hvk_bf16* dst = a.out + (size_t)window_token_row(g, b, wh, ww, WIN, tq) * C + h * 32 + 8 * gq;
+        ring_store(dst, v);
+      }
+    }
+    continue;
+#endif
+    float rn;
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      qf[i] = l2_normalize(qf[i], rn, sc2);  // q^ * scale * log2e: the MFMA applies the scale
+      kf[i] = l2_normalize(kf[i], rn);
+    }
+#pragma unroll
+    for (int qi = 0; qi < K::NT; ++qi) {
+      // one query tile live at a time, its bias reads inside the iteration (VGPR budget)
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      hvk_u32x2 br[K::NT][2];
+      ring_bias_read_q<K::TR, K::NT>(br, bta, qi);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      hvk_f32x4 s[K::NT];
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki) {
+        lds_fence(br[ki][0]);
+        lds_fence(br[ki][1]);
+        const hvk_f32x4 bb = {__uint_as_float(br[ki][0][0]), __uint_as_float(br[ki][0][1]),
+                              __uint_as_float(br[ki][1][0]), __uint_as_float(br[ki][1][1])};
+        s[ki] = hvk_mfma16(kf[ki], qf[qi], bb);
+      }
+      const int pq = 16 * qi + li;
+      if (edge_r || edge_c) {  // wave-uniform: only the last window row / column is masked
+        const int qy = pq / K::PW, qx = pq % K::PW;
+        uint32_t mreg = 0;  // keys in another shift region than this query (swinv2.py:357-388)
+        if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
+        if (edge_c) mreg |= (kband >> 16) ^ (qx >= WIN - g.shift ? 0xFFFFu : 0u);
+#pragma unroll
+        for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[ki][r] = fmaf((float)((mreg >> (ki * 4 + r)) & 1u), mask2, s[ki][r]);
+          }
+      }
+      // logits arrive shifted by the head bound M_h (bias table): no row max.  Padding keys
+      // hold finite logits here; their V rows and row-sum weights are zero.
+#pragma unroll
+      for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(s[ki][r]);
+      hvk_f32x4 o[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, osum = {0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c) {
+        const hvk_f32x4 a0 = s[2 * c];
+        const hvk_f32x4 a1 = (2 * c + 1 < K::NT) ? s[2 * c + 1] : hvk_f32x4{0, 0, 0, 0};
+        const uint4 pf = make_uint4(hvk_pack2(a0[0], a0[1]), hvk_pack2(a0[2], a0[3]),
+                                    hvk_pack2(a1[0], a1[1]), hvk_pack2(a1[2], a1[3]));
+        o[0] = hvk_mfma16(vt[c][0], pf, o[0]);
+        o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
+        osum = hvk_mfma16(ones[c], pf, osum);  // row sums of the (bf16) P over real keys
+      }
+      const int tq = grid_token<WIN, K::PW>(pq);
+      if (tq >= 0) {
+        const float inv = __builtin_amdgcn_rcpf(osum[0]);
+        const uint4 v = make_uint4(hvk_pack2(o[0][0] * inv, o[0][1] * inv),
+                                   hvk_pack2(o[0][2] * inv, o[0][3] * inv),
+                                   hvk_pack2(o[1][0] * inv, o[1][1] * inv),
+                                   hvk_pack2(o[1][2] * inv, o[1][3] * inv));
+        hvk_bf16* dst = a.out + (size_t)window_token_row(g, b, wh, ww, WIN, tq) * C + h * 32 + 8 * gq;
+        ring_store(dst, v);
+      }
+    }
+  }
+}
+
+template <int WIN, int HG>
+int launch_ring(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
+  using K = RingCfg<WIN, HG>;
+  const int per_cu = (160 * 1024) / K::LDS;
+  int rc = make_geom(B, H, W, C, nH, WIN, shift, 256 * per_cu * HG, a.g);  // capacity in groups*chunks
+  if (rc) return rc;
+  // make_geom sized chunks for nH "heads"; here the unit is a head GROUP
+  const int ng = nH / HG;
+  int chunks = 256 * per_cu / ng / 8 * 8;
+  if (chunks < 8) chunks = 8;
+  const int need = (a.g.n_windows + 7) / 8 * 8;
+  a.g.n_chunks = chunks < need ? chunks : need;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_ring_kernel<WIN, HG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+    attr = true;
+  }
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_ring_kernel<WIN, HG>), dim3(a.g.n_chunks * ng),
+                   dim3(64 * HG), K::LDS, st, a);
+  HVK_CHECK_LAUNCH("wmsa_fwd_ring");
+  return HVK_OK;
+}
+
+template <int WIN>
+int ring_win(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
+  // head group: HG heads per workgroup (the group's q/k/v slices are HG*64 contiguous bytes)
+  static const int force = [] {
+    const char* e = getenv("HVK_WMSA_FWD_HG");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 4 && nH % 4 == 0) return launch_ring<WIN, 4>(a, B, H, W, C, nH, shift, st);
+  if (force == 3 && nH % 3 == 0) return launch_ring<WIN, 3>(a, B, H, W, C, nH, shift, st);
+  if (force == 2 && nH % 2 == 0) return launch_ring<WIN, 2>(a, B, H, W, C, nH, shift, st);
+  if (nH % 3 == 0) return launch_ring<WIN, 3>(a, B, H, W, C, nH, shift, st);
+  if (nH % 4 == 0) return launch_ring<WIN, 4>(a, B, H, W, C, nH, shift, st);
+  if (nH % 2 == 0) return launch_ring<WIN, 2>(a, B, H, W, C, nH, shift, st);
+  return launch_ring<WIN, 1>(a, B, H, W, C, nH, shift, st);
+}
+
+}  // namespace
+
+namespace hvk_wmsa {
+int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st) {
+  switch (win) {
+    case 7: return ring_win<7>(a, B, H, W, C, nH, shift, st);
+    case 8: return ring_win<8>(a, B, H, W, C, nH, shift, st);
+    case 6: return ring_win<6>(a, B, H, W, C, nH, shift, st);
+    case 4: return ring_win<4>(a, B, H, W, C, nH, shift, st);
+    default: return hvk_set_error(HVK_EUNSUPPORTED, "wmsa ring: window %d", win);
+  }
+}
+}  // namespace hvk_wmsa
