@@ -224,7 +224,7 @@ def main():
         fwd_gbs = fwd_bytes * timed_steps / (fw_ms / 1000) / 1e9
         bwd_gbs = bwd_bytes * timed_steps / (bw_ms / 1000) / 1e9
         result["roofline"] = {
-            "kernel": "wmsa_fwd_kernel<7> (all %d launches per step)" % n_launch,
+            "kernel": "wmsa_fwd_ring_kernel<7,3|4> (all %d launches per step)" % n_launch,
             "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
             "algorithmic_bytes_per_step": fwd_bytes,
