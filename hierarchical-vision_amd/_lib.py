@@ -33,6 +33,8 @@ SIGNATURES = {
                          _p]),
     "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),

@@ -43,13 +43,18 @@ __device__ __forceinline__ int perm_row(int p) {
 // EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
 // bf16 pre-activation kept for the backward and the activation for fc2 (the reference's
 // F.linear(+bias) -> nn.GELU on the bf16 tensor, swinv2.py:58-62).
+// EPI 2 (fc2 input gradient through the activation): Y = gh = bf16(acc * GELU'(h)) with h
+// read from Y2 (the saved fc1 pre-activation), and csum[n] += sum over rows of gh (the fc1
+// bias gradient): per-lane register sums over the workgroup's row tiles, one 16-lane
+// shuffle reduction and one atomic per column and wave at the end.
 template <int K, int BN, int WAVES, bool PREF, bool BIAS, int EPI = 0>
 __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __restrict__ X,
                                                           const hvk_bf16* __restrict__ W,
                                                           const float* __restrict__ bias,
                                                           hvk_bf16* __restrict__ Y,
                                                           hvk_bf16* __restrict__ Y2, int M, int N,
-                                                          int ncb, int row_groups) {
+                                                          int ncb, int row_groups,
+                                                          float* __restrict__ csum = nullptr) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -92,6 +97,12 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
 
   uint4 xf[G::KS];
   load_x(tile, xf);
+  float cs[EPI == 2 ? G::NT / 2 : 1][8];
+  if (EPI == 2)
+#pragma unroll
+    for (int j = 0; j < G::NT / 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) cs[j][e] = 0.f;
   for (; tile < tiles; tile += stride) {
     // W never changes, but re-read its fragments from LDS every tile: hoisting them out of
     // the loop would pin KS x NT x 4 VGPRs (and spill)
@@ -117,6 +128,19 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           v[r] = acc[2 * j][r];
           v[4 + r] = acc[2 * j + 1][r];
         }
+        if (EPI == 2) {
+          float hv[8];
+          hvk_unpack8(hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j), hv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= hvk_gelu::gelu_grad(hv[e]);
+          const uint4 gv = hvk_pack8(v);
+          hvk_st16(yp + 32 * j, gv);
+          float r[8];
+          hvk_unpack8(gv, r);  // the bias gradient sums the stored (rounded) gradient
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs[j][e] += r[e];
+          continue;
+        }
         if (BIAS) {
           const float4 b0 = *reinterpret_cast<const float4*>(bl + 32 * j + 8 * g);
           const float4 b1 = *reinterpret_cast<const float4*>(bl + 32 * j + 8 * g + 4);
@@ -141,13 +165,24 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
       load_x(tile + stride, xf);
     }
   }
+  if (EPI == 2) {
+#pragma unroll
+    for (int j = 0; j < G::NT / 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float v = cs[j][e];
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m);
+        if (li == 0) atomicAdd(csum + n0 + 32 * j + 8 * g + e, v);
+      }
+  }
 }
 
 int g_cu_count = 0;
 
 template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
 int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
-                  int N, hipStream_t st, hvk_bf16* Y2 = nullptr) {
+                  int N, hipStream_t st, hvk_bf16* Y2 = nullptr, float* csum = nullptr) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
   auto kb = &linear_kernel<K, BN, WAVES, PREF, true, EPI>;
@@ -180,9 +215,11 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   if (row_groups < 8) row_groups = 8;
   const dim3 grid(row_groups * ncb);
   if (bias)
-    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups,
+                       csum);
   else
-    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups);
+    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups,
+                       csum);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }
@@ -264,6 +301,25 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   hvk_bf16* Yg = static_cast<hvk_bf16*>(y);
   if (K == 96) return launch_linear<96, 384, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+}
+
+int hvk_linear_gelu_bwd_supported(int M, int K, int N) {
+  return M > 0 && ((K == 96 && N == 384) || (K == 192 && N == 768));
+}
+
+int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias,
+                        int M, int K, int N, void* stream) {
+  if (!gy || !w || !h || !gh || !dbias)
+    return hvk_set_error(HVK_EINVAL, "hvk_linear_gelu_bwd: null pointer");
+  if (!hvk_linear_gelu_bwd_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_gelu_bwd: shape M=%d K=%d N=%d not built", M, K, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const hvk_bf16* X = static_cast<const hvk_bf16*>(gy);
+  const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
+  hvk_bf16* H = const_cast<hvk_bf16*>(static_cast<const hvk_bf16*>(h));
+  hvk_bf16* G = static_cast<hvk_bf16*>(gh);
+  if (K == 96) return launch_linear<96, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
+  return launch_linear<192, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
 }
 
 }  // extern "C"

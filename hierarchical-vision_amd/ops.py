@@ -372,6 +372,62 @@ def linear_gelu(x, weight, bias):
     return bias_gelu(linear(x, weight), bias)
 
 
+class MlpFn(torch.autograd.Function):
+    """fc2(GELU(fc1(x))) (swinv2.py:58-65 with drop = 0): forward = the fused fc1 + GELU kernel
+    and the fc2 GEMM; backward runs fc2's input gradient with the activation backward and the
+    fc1 bias gradient in ONE kernel (hvk_linear_gelu_bwd) instead of GEMM -> bf16 dy1 ->
+    activation kernel.  fc2's bias, when given, is added by the GEMM (else folded downstream)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        xb = _bf16(x)
+        w1b = w1.to(torch.bfloat16)
+        w2b = w2.to(torch.bfloat16)
+        N1, K = w1b.shape
+        x2 = xb.reshape(-1, K)
+        M = x2.shape[0]
+        h = torch.empty((M, N1), device=x.device, dtype=torch.bfloat16)
+        y1 = torch.empty_like(h)
+        call("hvk_linear_gelu_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(h), ptr(y1), M, K, N1,
+             stream())
+        y = mm_nt(y1, w2b, b2)
+        ctx.save_for_backward(xb, w1b, w2b, h, y1)
+        ctx.has_b2 = b2 is not None
+        return y.reshape(*xb.shape[:-1], w2b.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, w1b, w2b, h, y1 = ctx.saved_tensors
+        N1, K = w1b.shape
+        N2 = w2b.shape[0]
+        g2 = _bf16(gy).reshape(-1, N2)
+        M = g2.shape[0]
+        dw2 = weight_grad(g2, y1)
+        db2 = g2.sum(dim=0, dtype=torch.float32) if ctx.has_b2 else None
+        gh = torch.empty_like(h)
+        db1 = torch.zeros(N1, device=h.device, dtype=torch.float32)
+        call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2b.t().contiguous()), ptr(h), ptr(gh), ptr(db1),
+             M, N2, N1, stream())
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = (mm_nt(gh, w1b.t().contiguous()) if _linear_native(M, N1, K)
+                  else gh @ w1b).reshape(xb.shape)
+        dw1 = weight_grad(gh, xb.reshape(-1, K))
+        return gx, dw1, db1, dw2, db2
+
+
+def mlp(x, w1, b1, w2, b2=None):
+    """fc2(GELU(fc1(x))): the fused forward/backward kernels where built (stage 0-1 shapes),
+    else linear_gelu + linear."""
+    N1, K = w1.shape
+    M = x.numel() // K
+    lib = _lib.load()
+    if (b1 is not None and lib.hvk_linear_gelu_supported(M, K, N1)
+            and lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1)):
+        return MlpFn.apply(x, w1, b1, w2, b2)
+    return linear(linear_gelu(x, w1, b1), w2, b2)
+
+
 # --------------------------------------------------------------------------- PatchMerging
 class PatchMergeGather(torch.autograd.Function):
     """[B, H*W, C] -> [B, H/2*W/2, 4C] in the concat order of swinv2.py:486-490."""

@@ -118,6 +118,15 @@ class Mlp(nn.Module):
     def forward(self, x):
         return self.drop(ops.linear(self.hidden(x), self.fc2.weight, self.fc2.bias))
 
+    def forward_tokens(self, x, fc2_bias=True):
+        """forward() with fc2's bias optional (the caller may fold it into the next kernel);
+        fc1 + GELU + fc2 as one autograd node on the fused kernels when dropout is off."""
+        b2 = self.fc2.bias if fc2_bias else None
+        if (self.drop.p == 0 or not self.training) and isinstance(self.act, nn.GELU) \
+                and self.act.approximate == "none":
+            return ops.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, b2)
+        return self.drop(ops.linear(self.hidden(x), self.fc2.weight, b2))
+
     def hidden(self, x):
         """GELU(fc1(x)) with the bias add fused into the activation kernel."""
         if not isinstance(self.act, nn.GELU) or self.act.approximate != "none":
@@ -287,8 +296,7 @@ class SwinTransformerBlock(nn.Module):
         x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
                                         self.norm1.eps, abias=self.attn.proj_bias() if fold else None)
         fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
-        hid = self.mlp.hidden(xb)
-        h = self.mlp.drop(ops.linear(hid, self.mlp.fc2.weight, None if fold else self.mlp.fc2.bias))
+        h = self.mlp.forward_tokens(xb, fc2_bias=not fold)
         dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(h, x, self.norm2.weight, self.norm2.bias, dp, L,
                                         self.norm2.eps, abias=self.mlp.fc2.bias if fold else None)

@@ -82,6 +82,16 @@ int hvk_linear_gelu_supported(int M, int K, int N);
 int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                         int K, int N, void* stream);
 
+/* fc2 input gradient through the MLP activation (swinv2.py:58-65 backward): gh =
+ * bf16((gy w^T) * GELU'(h)) with gy: bf16 [M, K] (gradient of fc2's output), w: bf16 [N, K]
+ * (= fc2.weight^T), h: bf16 [M, N] (fc1's pre-activation saved by hvk_linear_gelu_fwd);
+ * dbias: f32 [N], ACCUMULATED into (+= column sums of gh = the fc1 bias gradient; the caller
+ * zeroes it).  Replaces the input-gradient GEMM + activation backward + bias reduction for
+ * the (K, N) shapes hvk_linear_gelu_bwd_supported() reports. */
+int hvk_linear_gelu_bwd_supported(int M, int K, int N);
+int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias, int M,
+                        int K, int N, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

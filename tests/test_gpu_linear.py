@@ -67,3 +67,40 @@ def test_linear_gelu_fused_matches_fp32(K, N):
                             ("dw", w.grad, wr.grad), ("db", b.grad, br.grad)]:
         rel = ((mine - ref).norm() / ref.norm()).item()
         assert rel < 1e-2, (name, rel)
+
+
+@pytest.mark.parametrize("C", [96, 192])
+@pytest.mark.parametrize("with_b2", [False, True])
+def test_mlp_fused_backward_matches_fp32(C, with_b2):
+    """fc2(GELU(fc1 x)) through the fused kernels (hvk_linear_gelu_fwd / _bwd) vs an fp32
+    autograd of the same bf16 operands: output, dx, dW1, db1, dW2, db2."""
+    from hvamd import _lib, ops
+    M, N1 = 3000, 4 * C
+    assert _lib.load().hvk_linear_gelu_bwd_supported(M, C, N1)
+    gen = torch.Generator(device="cuda").manual_seed(C)
+    x = torch.randn(M, C, device="cuda", generator=gen).bfloat16().requires_grad_(True)
+    w1 = (torch.randn(N1, C, device="cuda", generator=gen) / C ** 0.5).requires_grad_(True)
+    b1 = torch.randn(N1, device="cuda", generator=gen).requires_grad_(True)
+    w2 = (torch.randn(C, N1, device="cuda", generator=gen) / N1 ** 0.5).requires_grad_(True)
+    b2 = torch.randn(C, device="cuda", generator=gen).requires_grad_(True) if with_b2 else None
+    y = ops.mlp(x, w1, b1, w2, b2)
+    assert y.grad_fn is not None and "MlpFn" in type(y.grad_fn).__name__
+    gy = torch.randn(M, C, device="cuda", generator=gen).bfloat16()
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    w1r = w1.detach().bfloat16().float().requires_grad_(True)
+    b1r = b1.detach().clone().requires_grad_(True)
+    w2r = w2.detach().bfloat16().float().requires_grad_(True)
+    b2r = b2.detach().clone().requires_grad_(True) if with_b2 else None
+    yr = torch.nn.functional.gelu(xr @ w1r.t() + b1r) @ w2r.t()
+    if with_b2:
+        yr = yr + b2r
+    yr.backward(gy.float())
+    torch.cuda.synchronize()
+    pairs = [("y", y.float(), yr), ("dx", x.grad.float(), xr.grad), ("dw1", w1.grad, w1r.grad),
+             ("db1", b1.grad, b1r.grad), ("dw2", w2.grad, w2r.grad)]
+    if with_b2:
+        pairs.append(("db2", b2.grad, b2r.grad))
+    for name, mine, ref in pairs:
+        rel = ((mine - ref).norm() / ref.norm()).item()
+        assert rel < 2e-2, (name, rel)
