@@ -261,6 +261,9 @@ class LayerNormResidual(torch.autograd.Function):
         ctx.save_for_backward(a, abias, gamma, sample_scale, mean, rstd)
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
+        # an unused output (e.g. the bf16 copy at a stage end) gets None, not a zero-filled
+        # activation-sized gradient: the kernel takes NULL for either
+        ctx.set_materialize_grads(False)
         return x, xb
 
     @staticmethod

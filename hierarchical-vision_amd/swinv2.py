@@ -292,12 +292,15 @@ class SwinTransformerBlock(nn.Module):
         assert L == H * W, "input feature has wrong size"
         fold = self.attn.proj_drop.p == 0 or not self.training  # proj bias -> LN kernel
         a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold)
-        dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
+        planned = getattr(self, "_dp", None) if self.training else None  # from _plan_drop_path
+        if planned is not None and planned[0].shape[0] != B:
+            planned = None
+        dp = planned[0] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
                                         self.norm1.eps, abias=self.attn.proj_bias() if fold else None)
         fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
         h = self.mlp.forward_tokens(xb, fc2_bias=not fold)
-        dp = _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
+        dp = planned[1] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(h, x, self.norm2.weight, self.norm2.bias, dp, L,
                                         self.norm2.eps, abias=self.mlp.fc2.bias if fold else None)
         return ResidualStream(x, xb)
@@ -509,7 +512,28 @@ class SwinTransformerV2(nn.Module):
     def no_weight_decay_keywords(self):
         return {"cpb_mlp", "logit_scale", "relative_position_bias_table"}
 
+    def _plan_drop_path(self, batch, device):
+        """Draw every block's two DropPath masks for this forward in one shot ([2n, B]: one
+        rand + compare + scale instead of two bernoulli/div launches per residual branch).
+        Blocks reuse their pair on an activation-checkpoint recompute."""
+        blocks = [blk for layer in self.layers for blk in layer.blocks]
+        probs = [blk.drop_path_prob for blk in blocks]
+        if not self.training or max(probs, default=0.0) <= 0.0:
+            for blk in blocks:
+                blk._dp = None
+            return
+        key = (device, len(blocks))
+        if getattr(self, "_dp_keep", None) is None or self._dp_keep[0] != key:
+            keep = torch.tensor([1.0 - p for p in probs for _ in (0, 1)], dtype=torch.float32,
+                                device=device)
+            self._dp_keep = (key, keep)
+        keep = self._dp_keep[1][:, None]
+        scales = (torch.rand((2 * len(blocks), batch), device=device) < keep).float().div_(keep)
+        for i, blk in enumerate(blocks):
+            blk._dp = None if probs[i] <= 0.0 else (scales[2 * i], scales[2 * i + 1])
+
     def forward_features(self, x, output_activations=False):
+        self._plan_drop_path(x.shape[0], x.device)
         s = self.patch_embed.forward_stream(x)
         if self.ape:
             s = _as_stream(s.f32 + self.absolute_pos_embed)
