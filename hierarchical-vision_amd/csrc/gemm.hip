@@ -241,6 +241,10 @@ const LinCfg kLin[][4] = {
     {{192, 576, 288, 8, 1}, {192, 576, 288, 16, 1}, {192, 576, 288, 16, 0}, {192, 576, 192, 16, 1}},
     {{192, 768, 256, 8, 1}, {192, 768, 256, 16, 1}, {192, 768, 256, 16, 0}, {192, 768, 192, 16, 1}},
     {{384, 192, 192, 8, 1}, {384, 192, 192, 16, 1}, {384, 192, 192, 16, 0}, {384, 192, 96, 16, 1}},
+    // stage 2 (M = 50176): weight-stationary MFMA tiles instead of the library GEMM
+    {{384, 1152, 128, 8, 1}, {384, 1152, 64, 8, 1}, {384, 1152, 128, 16, 1}, {384, 1152, 64, 4, 1}},
+    {{384, 384, 128, 8, 1}, {384, 384, 64, 8, 1}, {384, 384, 128, 16, 1}, {384, 384, 64, 4, 1}},
+    {{384, 1536, 128, 8, 1}, {384, 1536, 64, 8, 1}, {384, 1536, 128, 16, 1}, {384, 1536, 64, 4, 1}},
 };
 
 const LinCfg* pick(int K, int N) {
@@ -277,7 +281,8 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
   HVK_LIN3(48, 96) HVK_LIN3(96, 96) HVK_LIN3(96, 288) HVK_LIN3(96, 384) HVK_LIN3(384, 96)
   HVK_LIN3(288, 96) HVK_LIN3(192, 192) HVK_LIN3(192, 288) HVK_LIN3(192, 256) HVK_LIN3(384, 192)
   HVK_LIN(96, 192, 16, 1) HVK_LIN(384, 96, 8, 0) HVK_LIN(288, 96, 8, 0) HVK_LIN(192, 96, 16, 1)
-  HVK_LIN(384, 96, 16, 1)
+  HVK_LIN(384, 96, 16, 1) HVK_LIN(384, 128, 8, 1) HVK_LIN(384, 128, 16, 1) HVK_LIN(384, 64, 8, 1)
+  HVK_LIN(384, 64, 4, 1)
 #undef HVK_LIN3
 #undef HVK_LIN
   return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);
@@ -285,8 +290,9 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
 
 int hvk_linear_gelu_supported(int M, int K, int N) {
   const LinCfg* c = pick(K, N);
-  return M > 0 && c && ((c->K == 96 && c->BN == 384) || (c->K == 192 && c->BN == 256)) &&
-         c->waves == 8 && c->pref == 1;
+  return M > 0 && c &&
+         ((c->K == 96 && c->BN == 384) || (c->K == 192 && c->BN == 256) || (c->K == 384 && c->BN == 128)) &&
+         c->N == 4 * c->K && c->waves == 8 && c->pref == 1;
 }
 
 int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
@@ -300,11 +306,12 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   hvk_bf16* H = static_cast<hvk_bf16*>(h);
   hvk_bf16* Yg = static_cast<hvk_bf16*>(y);
   if (K == 96) return launch_linear<96, 384, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+  if (K == 384) return launch_linear<384, 128, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
 }
 
 int hvk_linear_gelu_bwd_supported(int M, int K, int N) {
-  return M > 0 && ((K == 96 && N == 384) || (K == 192 && N == 768));
+  return M > 0 && ((K == 96 && N == 384) || (K == 192 && N == 768) || (K == 384 && N == 1536));
 }
 
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias,
@@ -319,6 +326,7 @@ int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, 
   hvk_bf16* H = const_cast<hvk_bf16*>(static_cast<const hvk_bf16*>(h));
   hvk_bf16* G = static_cast<hvk_bf16*>(gh);
   if (K == 96) return launch_linear<96, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
+  if (K == 384) return launch_linear<384, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
   return launch_linear<192, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
 }
 

@@ -5,7 +5,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(48, 96), (96, 96), (96, 288), (96, 384), (384, 96), (288, 96), (192, 192), (192, 576),
-          (192, 768), (384, 192)]
+          (192, 768), (384, 192), (384, 1152), (384, 384), (384, 1536)]
 
 
 @pytest.mark.parametrize("K,N", SHAPES)
@@ -45,7 +45,7 @@ def test_linear_autograd_uses_native_and_matches():
         assert rel < 1e-2, rel
 
 
-@pytest.mark.parametrize("K,N", [(96, 384), (192, 768)])
+@pytest.mark.parametrize("K,N", [(96, 384), (192, 768), (384, 1536)])
 def test_linear_gelu_fused_matches_fp32(K, N):
     from hvamd import _lib, ops
     M = 3000
@@ -69,7 +69,7 @@ def test_linear_gelu_fused_matches_fp32(K, N):
         assert rel < 1e-2, (name, rel)
 
 
-@pytest.mark.parametrize("C", [96, 192])
+@pytest.mark.parametrize("C", [96, 192, 384])
 @pytest.mark.parametrize("with_b2", [False, True])
 def test_mlp_fused_backward_matches_fp32(C, with_b2):
     """fc2(GELU(fc1 x)) through the fused kernels (hvk_linear_gelu_fwd / _bwd) vs an fp32
