@@ -33,6 +33,9 @@ SIGNATURES = {
                          _p]),
     "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_gemm_supported": (_i, [_i, _i, _i]),
+    "hvk_gemm_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_gemm_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),

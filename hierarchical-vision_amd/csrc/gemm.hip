@@ -95,8 +95,19 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     }
   };
 
+  // EPI 2: the saved pre-activation of the row tile, prefetched one tile ahead like X
+  auto load_h = [&](int t, uint4 (&hf)[EPI == 2 ? G::NT / 2 : 1]) {
+    if (EPI != 2) return;
+    const int row = 16 * t + li;
+    const bool ok = t < tiles && row < M;
+#pragma unroll
+    for (int j = 0; j < G::NT / 2; ++j)
+      hf[j] = ok ? hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j) : make_uint4(0, 0, 0, 0);
+  };
   uint4 xf[G::KS];
   load_x(tile, xf);
+  uint4 hf[EPI == 2 ? G::NT / 2 : 1];
+  load_h(tile, hf);
   float cs[EPI == 2 ? G::NT / 2 : 1][8];
   if (EPI == 2)
 #pragma unroll
@@ -109,6 +120,8 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     asm volatile("" ::: "memory");
     uint4 xn[G::KS];
     if (PREF) load_x(tile + stride, xn);
+    uint4 hn[EPI == 2 ? G::NT / 2 : 1];
+    load_h(tile + stride, hn);
     hvk_f32x4 acc[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
@@ -130,7 +143,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
         }
         if (EPI == 2) {
           float hv[8];
-          hvk_unpack8(hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j), hv);
+          hvk_unpack8(hf[EPI == 2 ? j : 0], hv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= hvk_gelu::gelu_grad(hv[e]);
           const uint4 gv = hvk_pack8(v);
@@ -158,6 +171,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
         }
       }
     }
+    if (EPI == 2)
+#pragma unroll
+      for (int j = 0; j < G::NT / 2; ++j) hf[j] = hn[j];
     if (PREF) {
 #pragma unroll
       for (int s = 0; s < G::KS; ++s) xf[s] = xn[s];
@@ -241,10 +257,9 @@ const LinCfg kLin[][4] = {
     {{192, 576, 288, 8, 1}, {192, 576, 288, 16, 1}, {192, 576, 288, 16, 0}, {192, 576, 192, 16, 1}},
     {{192, 768, 256, 8, 1}, {192, 768, 256, 16, 1}, {192, 768, 256, 16, 0}, {192, 768, 192, 16, 1}},
     {{384, 192, 192, 8, 1}, {384, 192, 192, 16, 1}, {384, 192, 192, 16, 0}, {384, 192, 96, 16, 1}},
-    // stage 2 (M = 50176): weight-stationary MFMA tiles instead of the library GEMM
-    {{384, 1152, 128, 8, 1}, {384, 1152, 64, 8, 1}, {384, 1152, 128, 16, 1}, {384, 1152, 64, 4, 1}},
-    {{384, 384, 128, 8, 1}, {384, 384, 64, 8, 1}, {384, 384, 128, 16, 1}, {384, 384, 64, 4, 1}},
-    {{384, 1536, 128, 8, 1}, {384, 1536, 64, 8, 1}, {384, 1536, 128, 16, 1}, {384, 1536, 64, 4, 1}},
+    // stage 2 fc2 input gradient with the GELU backward (EPI 2); plain stage-2 GEMMs run on the
+    // tiled kernel (gemm_tile.hip)
+    {{384, 1536, 128, 8, 1}, {384, 1536, 64, 8, 1}, {384, 1536, 128, 8, 1}, {384, 1536, 64, 4, 1}},
 };
 
 const LinCfg* pick(int K, int N) {
@@ -281,8 +296,7 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
   HVK_LIN3(48, 96) HVK_LIN3(96, 96) HVK_LIN3(96, 288) HVK_LIN3(96, 384) HVK_LIN3(384, 96)
   HVK_LIN3(288, 96) HVK_LIN3(192, 192) HVK_LIN3(192, 288) HVK_LIN3(192, 256) HVK_LIN3(384, 192)
   HVK_LIN(96, 192, 16, 1) HVK_LIN(384, 96, 8, 0) HVK_LIN(288, 96, 8, 0) HVK_LIN(192, 96, 16, 1)
-  HVK_LIN(384, 96, 16, 1) HVK_LIN(384, 128, 8, 1) HVK_LIN(384, 128, 16, 1) HVK_LIN(384, 64, 8, 1)
-  HVK_LIN(384, 64, 4, 1)
+  HVK_LIN(384, 96, 16, 1) HVK_LIN(384, 128, 8, 1) HVK_LIN(384, 64, 8, 1) HVK_LIN(384, 64, 4, 1)
 #undef HVK_LIN3
 #undef HVK_LIN
   return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);

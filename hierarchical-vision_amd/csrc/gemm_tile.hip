@@ -1,0 +1,228 @@
+// Tiled MFMA GEMM for the compute-heavier SwinV2 Linears on gfx950 (stage 2-3 of SwinV2-T:
+// M = 12544-50176 tokens, K = 384-3072, N = 384-3072), where the weight block no longer fits
+// the skinny kernel's LDS (gemm.hip):
+//   Y[M, N] = X[M, K] W[N, K]^T (+ bias[N]) (EPI 0), or the fc1 form h = Y + bias, GELU(h)
+//   (EPI 1) -- F.linear of swinv2.py:58-62, 220, 262 and the input gradients (W = weight^T).
+// 128 x 128 output tile per 256-thread workgroup (2 x 2 waves of 64 x 64), K in steps of 64:
+//  * both operand tiles are staged by LDS-DMA (global_load_lds_dwordx4, nontemporal off),
+//    each wave-instruction moving 8 whole 128-B row segments; two buffers, the next k-step's
+//    DMA in flight during the current MFMAs (counted vmcnt, raw s_barrier);
+//  * LDS rows are 128 B with the 16-B chunk index XOR-swizzled by (row & 7): the fragment
+//    reads (ds_read_b128, 16 rows x 16 B per lane group) are bank-conflict free; the swizzle
+//    is applied on the DMA's global source address (the LDS side of a DMA is lane-linear);
+//  * Y^T = W X^T on v_mfma_f32_16x16x32_bf16 with the W rows of each 32-row pair permuted
+//    (as gemm.hip), so a lane ends with 8 consecutive output columns of one row: 16-B stores.
+#include <stdlib.h>
+
+#include "hvk_common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_vptr_t;
+typedef __attribute__((address_space(1))) void* gbl_vptr_t;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;  // double buffered: 64 KB
+
+// LDS row p of a W tile holds W row perm(p) of the tile (see gemm.hip: the accumulator rows
+// 4g + r of tiles 2j, 2j+1 then map to output columns 32j + 8g .. 32j + 8g + 7)
+__device__ __forceinline__ int perm_row(int p) {
+  const int t = p >> 4, m = p & 15;
+  return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
+}
+
+// byte offset in a [128][64] bf16 tile of the 16-B chunk c of row r (swizzled)
+__device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+// fragment reads from inline asm: hipcc would otherwise wait vmcnt(0) before every LDS read
+// while the next k-step's DMA is in flight (cdna_hip_programming.md, glds pipelining)
+template <int OFF>
+__device__ __forceinline__ hvk_u32x4 rd128(uint32_t a) {
+  hvk_u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+__device__ __forceinline__ uint4 tie(hvk_u32x4 v) {
+  asm volatile("" : "+v"(v));
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
+                                                        const hvk_bf16* __restrict__ Wt,
+                                                        const float* __restrict__ bias,
+                                                        hvk_bf16* __restrict__ Y,
+                                                        hvk_bf16* __restrict__ Y2, int M, int N,
+                                                        int K, int mtiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntiles = N / BN;
+  // XCD-aware decode: the n-tiles of one m-tile share blockIdx % 8 (one L2): the X row block
+  // is fetched from HBM once and re-read from L2
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int nt = loc % ntiles, mt = (loc / ntiles) * 8 + xcd;
+  if (mt >= mtiles) return;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  const int wn = wave & 1, wm = wave >> 1;  // this wave's 64 x 64 sub-tile (n half, m half)
+  const int KT = K / BK;
+
+  // DMA: tile operand instruction j (0..15) fills LDS rows 8j .. 8j+7; lane L -> row
+  // 8j + L/8, LDS chunk L%8 <- global chunk (L%8) ^ (row & 7).  Wave w issues j = w + 4i.
+  const int lr = lane >> 3, lc = lane & 7;
+  size_t xsrc[4], wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * (wave + 4 * i) + lr;
+    const int gc = lc ^ (row & 7);
+    int xr = m0 + row;
+    if (xr >= M) xr = M - 1;  // rows past M: any valid row (never stored)
+    xsrc[i] = (size_t)xr * K + 8 * gc;
+    wsrc[i] = (size_t)(n0 + perm_row(row)) * K + 8 * gc;
+  }
+  auto issue = [&](int kt, int buf) {
+    char* base = smem + buf * STAGE_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = wave + 4 * i;
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(Wt + wsrc[i] + k0), (lds_vptr_t)(base + j * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + xsrc[i] + k0),
+                                       (lds_vptr_t)(base + TILE_BYTES + j * 1024), 16, 0, 0);
+    }
+  };
+
+  hvk_f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = hvk_f32x4{0, 0, 0, 0};
+
+  issue(0, 0);
+  if (KT > 1) issue(1, 1);
+  for (int kt = 0; kt < KT; ++kt) {
+    // this k-step's tile has landed (the next one's 8 DMAs per wave may stay in flight)
+    if (kt + 1 < KT)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const uint32_t base = lds_u32(smem) + (kt & 1) * STAGE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // rows 64w + 16t + li (row & 7 = li & 7), chunk 4ks + g swizzled; t in immediates
+      const uint32_t aw = base + (64 * wn + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
+      const uint32_t ax = base + TILE_BYTES + (64 * wm + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
+      hvk_u32x4 ra[4], rb[4];
+      ra[0] = rd128<0>(aw);
+      ra[1] = rd128<2048>(aw);
+      ra[2] = rd128<4096>(aw);
+      ra[3] = rd128<6144>(aw);
+      rb[0] = rd128<0>(ax);
+      rb[1] = rd128<2048>(ax);
+      rb[2] = rd128<4096>(ax);
+      rb[3] = rd128<6144>(ax);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint4 af[4], bf[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        af[t] = tie(ra[t]);
+        bf[t] = tie(rb[t]);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = hvk_mfma16(af[a], bf[b], acc[a][b]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done with this buffer
+    asm volatile("" ::: "memory");
+    if (kt + 2 < KT) issue(kt + 2, kt & 1);
+  }
+
+  // epilogue: lane (li, g) holds, for m-tile b and n-tile pair (2j, 2j+1), row
+  // m0 + 64wm + 16b + li and columns n0 + 64wn + 32j + 8g .. +7
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int row = m0 + 64 * wm + 16 * b + li;
+    if (row >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + 64 * wn + 32 * j + 8 * g;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[2 * j][b][r];
+        v[4 + r] = acc[2 * j + 1][b][r];
+      }
+      if (bias) {
+        const float4 b0 = *reinterpret_cast<const float4*>(bias + col);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias + col + 4);
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      const uint4 hv = hvk_pack8(v);
+      *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hv;
+      if (EPI == 1) {
+        float u[8];
+        hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
+#pragma unroll
+        for (int e = 0; e < 8; ++e) u[e] = hvk_gelu::gelu(u[e]);
+        *reinterpret_cast<uint4*>(Y2 + (size_t)row * N + col) = hvk_pack8(u);
+      }
+    }
+  }
+}
+
+template <int EPI>
+int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
+                int M, int N, int K, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    attr = true;
+  }
+  const int mtiles = (M + BM - 1) / BM;
+  const int mpad = (mtiles + 7) / 8 * 8;
+  const dim3 grid(mpad * (N / BN));
+  hipLaunchKernelGGL(gemm_nt_kernel<EPI>, grid, dim3(256), LDS_BYTES, st, X, W, bias, Y, Y2, M, N, K,
+                     mtiles);
+  HVK_CHECK_LAUNCH("hvk_gemm_tile");
+  return HVK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hvk_gemm_supported(int M, int K, int N) {
+  return M > 0 && K >= BK && K % BK == 0 && N % BN == 0 && K <= 8192 && N <= 16384;
+}
+
+int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
+                 void* stream) {
+  if (!x || !w || !y) return hvk_set_error(HVK_EINVAL, "hvk_gemm_fwd: null pointer");
+  if (!hvk_gemm_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_fwd: M=%d K=%d N=%d (K %% 64, N %% 128)", M, K, N);
+  return launch_tile<0>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
+                        static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream));
+}
+
+int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M, int K,
+                      int N, void* stream) {
+  if (!x || !w || !h || !y || !bias) return hvk_set_error(HVK_EINVAL, "hvk_gemm_gelu_fwd: null pointer");
+  if (!hvk_gemm_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_gelu_fwd: M=%d K=%d N=%d", M, K, N);
+  return launch_tile<1>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
+                        static_cast<hvk_bf16*>(h), static_cast<hvk_bf16*>(y), M, N, K,
+                        static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -78,11 +78,50 @@ def _linear_native(M, K, N):
     return ok and M > 0
 
 
-def mm_nt(x2, wb, bias=None):
-    """y = x2 wb^T (+ bias): libhvk's MFMA kernel where built, else the library GEMM (the
-    compute-bound stage 2-3 shapes).  x2 [M, K] bf16, wb [N, K] bf16, bias f32 [N]."""
+def _tile_ok(M, K, N):
+    """libhvk's tiled MFMA GEMM (hvk_gemm_fwd) where it measured faster than the library GEMM
+    (tools/bench_skinny.py): the stage-2 shapes with K <= 1152 and the 768 x 768 stage-3
+    projection; the wider stage-3 shapes stay on the library."""
+    if K % 64 or N % 128 or M <= 0:
+        return False
+    return (M >= 32768 and K <= 1152) or (K == 768 and N == 768)
+
+
+def _native_nt(M, K, N):
+    """True when mm_nt runs one of libhvk's GEMMs for this shape."""
+    return _tile_ok(M, K, N) or _linear_native(M, K, N)
+
+
+def gelu_fwd(x2, wb, bias):
+    """(h, GELU(h)) with h = x2 wb^T + bias as ONE kernel (fc1 of swinv2.py:58-62), or None
+    when no fused kernel is built for the shape."""
     M, K = x2.shape
     N = wb.shape[0]
+    lib = _lib.load()
+    if K in (96, 192) and lib.hvk_linear_gelu_supported(M, K, N):
+        fn = "hvk_linear_gelu_fwd"
+    elif _tile_ok(M, K, N):
+        fn = "hvk_gemm_gelu_fwd"
+    else:
+        return None
+    h = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
+    y = torch.empty_like(h)
+    call(fn, ptr(x2), ptr(wb), ptr(_f32(bias)), ptr(h), ptr(y), M, K, N, stream())
+    return h, y
+
+
+def mm_nt(x2, wb, bias=None):
+    """y = x2 wb^T (+ bias): libhvk's MFMA kernels where built (skinny weight-stationary for
+    the memory-bound stage 0-1 shapes, tiled for stage 2), else the library GEMM.  x2 [M, K]
+    bf16, wb [N, K] bf16, bias f32 [N]."""
+    M, K = x2.shape
+    N = wb.shape[0]
+    if _tile_ok(M, K, N):
+        y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
+        b = _f32(bias) if bias is not None else None
+        call("hvk_gemm_fwd", ptr(x2), ptr(wb), ptr(b) if b is not None else None, ptr(y), M, K, N,
+             stream())
+        return y
     if _linear_native(M, K, N):
         y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
         b = _f32(bias) if bias is not None else None
@@ -114,7 +153,7 @@ class LinearFn(torch.autograd.Function):
         g2 = _bf16(gy).reshape(-1, N)
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(g2, wb.t().contiguous()) if _linear_native(g2.shape[0], N, K)
+            gx = (mm_nt(g2, wb.t().contiguous()) if _native_nt(g2.shape[0], N, K)
                   else g2 @ wb).reshape(xb.shape)
         dw = weight_grad(g2, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
         db = g2.sum(dim=0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
@@ -328,21 +367,16 @@ def bias_gelu(h, bias):
 
 
 class LinearGelu(torch.autograd.Function):
-    """y = GELU(x W^T + b) as ONE kernel (hvk_linear_gelu_fwd: fc1 GEMM with the bias + GELU
-    epilogue, writing the bf16 pre-activation h for the backward); backward = the activation
-    backward on h (db = its column sums) + the Linear backward."""
+    """y = GELU(x W^T + b) as ONE kernel (gelu_fwd: fc1 GEMM with the bias + GELU epilogue,
+    writing the bf16 pre-activation h for the backward); backward = the activation backward on
+    h (db = its column sums) + the Linear backward."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         xb = _bf16(x)
         wb = weight.to(torch.bfloat16)
         N, K = wb.shape
-        x2 = xb.reshape(-1, K)
-        M = x2.shape[0]
-        h = torch.empty((M, N), device=x.device, dtype=torch.bfloat16)
-        y = torch.empty_like(h)
-        call("hvk_linear_gelu_fwd", ptr(x2), ptr(wb), ptr(_f32(bias)), ptr(h), ptr(y), M, K, N,
-             stream())
+        h, y = gelu_fwd(xb.reshape(-1, K), wb, bias)
         ctx.save_for_backward(xb, wb, h)
         return y.reshape(*xb.shape[:-1], N)
 
@@ -360,7 +394,7 @@ class LinearGelu(torch.autograd.Function):
              stream())
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(gh, wb.t().contiguous()) if _linear_native(M, N, K)
+            gx = (mm_nt(gh, wb.t().contiguous()) if _native_nt(M, N, K)
                   else gh @ wb).reshape(xb.shape)
         dw = weight_grad(gh, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
         return gx, dw, db
@@ -368,9 +402,10 @@ class LinearGelu(torch.autograd.Function):
 
 def linear_gelu(x, weight, bias):
     """GELU(F.linear(x, weight, bias)): fused kernel where built, else GEMM + activation kernel."""
-    K = weight.shape[1]
+    N, K = weight.shape
     M = x.numel() // K
-    if bias is not None and _lib.load().hvk_linear_gelu_supported(M, K, weight.shape[0]):
+    if bias is not None and ((K in (96, 192) and _lib.load().hvk_linear_gelu_supported(M, K, N))
+                             or _tile_ok(M, K, N)):
         return LinearGelu.apply(x, weight, bias)
     return bias_gelu(linear(x, weight), bias)
 
@@ -389,10 +424,7 @@ class MlpFn(torch.autograd.Function):
         N1, K = w1b.shape
         x2 = xb.reshape(-1, K)
         M = x2.shape[0]
-        h = torch.empty((M, N1), device=x.device, dtype=torch.bfloat16)
-        y1 = torch.empty_like(h)
-        call("hvk_linear_gelu_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(h), ptr(y1), M, K, N1,
-             stream())
+        h, y1 = gelu_fwd(x2, w1b, b1)
         y = mm_nt(y1, w2b, b2)
         ctx.save_for_backward(xb, w1b, w2b, h, y1)
         ctx.has_b2 = b2 is not None
@@ -413,7 +445,7 @@ class MlpFn(torch.autograd.Function):
              M, N2, N1, stream())
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(gh, w1b.t().contiguous()) if _linear_native(M, N1, K)
+            gx = (mm_nt(gh, w1b.t().contiguous()) if _native_nt(M, N1, K)
                   else gh @ w1b).reshape(xb.shape)
         dw1 = weight_grad(gh, xb.reshape(-1, K))
         return gx, dw1, db1, dw2, db2
@@ -425,7 +457,8 @@ def mlp(x, w1, b1, w2, b2=None):
     N1, K = w1.shape
     M = x.numel() // K
     lib = _lib.load()
-    if (b1 is not None and lib.hvk_linear_gelu_supported(M, K, N1)
+    if (b1 is not None and ((K in (96, 192) and lib.hvk_linear_gelu_supported(M, K, N1))
+                            or _tile_ok(M, K, N1))
             and lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1)):
         return MlpFn.apply(x, w1, b1, w2, b2)
     return linear(linear_gelu(x, w1, b1), w2, b2)

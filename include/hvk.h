@@ -92,6 +92,17 @@ int hvk_linear_gelu_bwd_supported(int M, int K, int N);
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias, int M,
                         int K, int N, void* stream);
 
+/* ---- Tiled MFMA GEMM (compute-heavier Linears) ----------------------------------------
+ * y[M, N] = x[M, K] w[N, K]^T (+ bias[N]) for K % 64 == 0, N % 128 == 0 (SwinV2 stage 2-3
+ * shapes: F.linear of swinv2.py:58-62, 220, 262, 492 and, with w = weight^T, their input
+ * gradients).  x, w, y bf16; bias f32 or NULL.  The _gelu form is fc1 (swinv2.py:58-62):
+ * h = bf16(x w^T + bias), y = GELU(h) (exact erf), bias required. */
+int hvk_gemm_supported(int M, int K, int N);
+int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
+                 void* stream);
+int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
+                      int K, int N, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

@@ -40,10 +40,20 @@ def main():
             err = ((y.float() - ref).norm() / ref.norm()).item()
         else:
             err = float("nan")
+        t_t = float("nan")
+        if lib.hvk_gemm_supported(M, K, N):
+            y2 = torch.empty_like(y)
+            t_t = timeit(lambda: _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), None, _lib.ptr(y2),
+                                           M, K, N, _lib.stream()))
+            ref = x.float() @ w.float().t()
+            err2 = ((y2.float() - ref).norm() / ref.norm()).item()
+        else:
+            err2 = float("nan")
         t_l = timeit(lambda: torch.nn.functional.linear(x, w))
         hbm = (M * K + M * N + N * K) * 2 / 5.5e12 * 1e6
         mf = 2 * M * K * N / 2.5e15 * 1e6
-        print(f"v{v} M={M} K={K} N={N}: hvk {t_h:7.1f} us (rel err {err:.1e})  lib {t_l:7.1f} us  "
+        print(f"v{v} M={M} K={K} N={N}: hvk {t_h:7.1f} us (rel err {err:.1e})  tile {t_t:7.1f} us "
+              f"(rel err {err2:.1e})  lib {t_l:7.1f} us  "
               f"floors hbm {hbm:5.1f} mfma {mf:5.1f}", flush=True)
 
 
