@@ -33,9 +33,6 @@ __device__ __forceinline__ int perm_row(int p) {
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
-// byte offset in a [128][64] bf16 tile of the 16-B chunk c of row r (swizzled)
-__device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
-
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -52,7 +49,7 @@ __device__ __forceinline__ uint4 tie(hvk_u32x4 v) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-template <int EPI>
+template <int EPI, bool PIPE>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
                                                         const hvk_bf16* __restrict__ Wt,
                                                         const float* __restrict__ bias,
@@ -114,31 +111,49 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const uint32_t base = lds_u32(smem) + (kt & 1) * STAGE_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    // PIPE: all 16 fragments of the k-step in flight at once, the first half's MFMAs start as
+    // soon as their 8 reads are back (lgkmcnt counts in issue order); else read-wait-compute
+    // per half
+    hvk_u32x4 ra[2][4], rb[2][4];
+    auto read_half = [&](int ks) {
       // rows 64w + 16t + li (row & 7 = li & 7), chunk 4ks + g swizzled; t in immediates
       const uint32_t aw = base + (64 * wn + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
       const uint32_t ax = base + TILE_BYTES + (64 * wm + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
-      hvk_u32x4 ra[4], rb[4];
-      ra[0] = rd128<0>(aw);
-      ra[1] = rd128<2048>(aw);
-      ra[2] = rd128<4096>(aw);
-      ra[3] = rd128<6144>(aw);
-      rb[0] = rd128<0>(ax);
-      rb[1] = rd128<2048>(ax);
-      rb[2] = rd128<4096>(ax);
-      rb[3] = rd128<6144>(ax);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ra[ks][0] = rd128<0>(aw);
+      ra[ks][1] = rd128<2048>(aw);
+      ra[ks][2] = rd128<4096>(aw);
+      ra[ks][3] = rd128<6144>(aw);
+      rb[ks][0] = rd128<0>(ax);
+      rb[ks][1] = rd128<2048>(ax);
+      rb[ks][2] = rd128<4096>(ax);
+      rb[ks][3] = rd128<6144>(ax);
+    };
+    auto mfma_half = [&](int ks) {
       uint4 af[4], bf[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        af[t] = tie(ra[t]);
-        bf[t] = tie(rb[t]);
+        af[t] = tie(ra[ks][t]);
+        bf[t] = tie(rb[ks][t]);
       }
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = hvk_mfma16(af[a], bf[b], acc[a][b]);
+    };
+    if (PIPE) {
+      read_half(0);
+      read_half(1);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      mfma_half(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      mfma_half(1);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        read_half(ks);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        mfma_half(ks);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave is done with this buffer
@@ -180,22 +195,37 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   }
 }
 
-template <int EPI>
-int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
+static bool tile_pipe() {
+  static const int v = [] {
+    const char* e = getenv("HVK_TILE_PIPE");
+    return e ? atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+template <int EPI, bool PIPE>
+int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                 int M, int N, int K, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, PIPE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
   const int mtiles = (M + BM - 1) / BM;
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / BN));
-  hipLaunchKernelGGL(gemm_nt_kernel<EPI>, grid, dim3(256), LDS_BYTES, st, X, W, bias, Y, Y2, M, N, K,
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, PIPE>), grid, dim3(256), LDS_BYTES, st, X, W, bias, Y, Y2, M, N, K,
                      mtiles);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
+}
+
+template <int EPI>
+int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
+                int M, int N, int K, hipStream_t st) {
+  return tile_pipe() ? launch_tile_<EPI, true>(X, W, bias, Y, Y2, M, N, K, st)
+                     : launch_tile_<EPI, false>(X, W, bias, Y, Y2, M, N, K, st);
 }
 
 }  // namespace

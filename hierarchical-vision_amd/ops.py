@@ -49,20 +49,31 @@ def _split_k_chunks(rows):
     return nc
 
 
-def weight_grad(g, x):
-    """dW = g^T x in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to ~10^6) and
-    N, K small: the library picks ~50 workgroups for this shape, so split the token
-    reduction into a batched GEMM over chunks (thousands of workgroups) + a small sum.
-    (A token-sliced MFMA kernel with f32 atomics was measured slower on every SwinV2-T shape:
-    with one 32-token chunk in flight per workgroup it is HBM-latency bound)"""
-    M = g.shape[0]
+def weight_grad(g, x, with_db=False):
+    """(dW, db) = (g^T x, g.sum(0)) in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to
+    ~10^6): libhvk's token-chunked MFMA kernel with the bias gradient fused (hvk_weight_grad,
+    one pass over g) for every SwinV2-T shape it is built for; otherwise the library GEMM
+    batched over token chunks (thousands of workgroups) + a small sum.  db is None unless
+    with_db."""
+    M, N = g.shape
+    K = x.shape[1]
+    lib = _lib.load()
+    if lib.hvk_weight_grad_supported(M, N, K):
+        dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
+        db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
+        nb = lib.hvk_weight_grad_workspace(M, N, K)
+        ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
+        call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
+             ptr(ws), nb, stream())
+        return dw, db
+    db = g.sum(dim=0, dtype=torch.float32) if with_db else None
     nc = _split_k_chunks(M)
     if nc == 1:
-        return torch.mm(g.t(), x, out_dtype=torch.float32)
+        return torch.mm(g.t(), x, out_dtype=torch.float32), db
     kc = M // nc
     part = torch.bmm(g.view(nc, kc, -1).transpose(1, 2), x.view(nc, kc, -1),
                      out_dtype=torch.float32)
-    return part.sum(dim=0)
+    return part.sum(dim=0), db
 
 
 _LIN_OK = {}
@@ -155,8 +166,12 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(g2, wb.t().contiguous()) if _native_nt(g2.shape[0], N, K)
                   else g2 @ wb).reshape(xb.shape)
-        dw = weight_grad(g2, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
-        db = g2.sum(dim=0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        dw, db = None, None
+        if ctx.needs_input_grad[1]:
+            dw, db = weight_grad(g2, xb.reshape(-1, K), want_db)
+        elif want_db:
+            db = g2.sum(dim=0, dtype=torch.float32)
         return gx, dw, db
 
 
@@ -396,7 +411,7 @@ class LinearGelu(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, wb.t().contiguous()) if _native_nt(M, N, K)
                   else gh @ wb).reshape(xb.shape)
-        dw = weight_grad(gh, xb.reshape(-1, K)) if ctx.needs_input_grad[1] else None
+        dw = weight_grad(gh, xb.reshape(-1, K))[0] if ctx.needs_input_grad[1] else None
         return gx, dw, db
 
 
@@ -437,8 +452,7 @@ class MlpFn(torch.autograd.Function):
         N2 = w2b.shape[0]
         g2 = _bf16(gy).reshape(-1, N2)
         M = g2.shape[0]
-        dw2 = weight_grad(g2, y1)
-        db2 = g2.sum(dim=0, dtype=torch.float32) if ctx.has_b2 else None
+        dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
         db1 = torch.zeros(N1, device=h.device, dtype=torch.float32)
         call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2b.t().contiguous()), ptr(h), ptr(gh), ptr(db1),
@@ -447,7 +461,7 @@ class MlpFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, w1b.t().contiguous()) if _native_nt(M, N1, K)
                   else gh @ w1b).reshape(xb.shape)
-        dw1 = weight_grad(gh, xb.reshape(-1, K))
+        dw1 = weight_grad(gh, xb.reshape(-1, K))[0]
         return gx, dw1, db1, dw2, db2
 
 

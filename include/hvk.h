@@ -103,6 +103,18 @@ int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                       int K, int N, void* stream);
 
+/* ---- Weight-gradient GEMM (the backward of every SwinV2 Linear) ----------------------
+ * dw[N, K] = g[M, N]^T x[M, K] in f32 and, when db is not NULL, db[N] = sum_m g[m, n]
+ * (F.linear backward of swinv2.py:58-62, 220, 262, 296; torch computes them as
+ * grad_output^T input and grad_output.sum(0)).  g, x bf16, token-major; dw, db f32,
+ * OVERWRITTEN.  M = tokens (M % 32 == 0); the (N, K) shapes hvk_weight_grad_supported()
+ * reports.  ws: device scratch of at least hvk_weight_grad_workspace(M, N, K) bytes (the
+ * per-chunk partial sums). */
+int hvk_weight_grad_supported(int M, int N, int K);
+size_t hvk_weight_grad_workspace(int M, int N, int K);
+int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
+                    void* ws, size_t ws_bytes, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

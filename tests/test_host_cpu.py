@@ -29,6 +29,11 @@ def test_library_exports_every_declared_symbol():
     # [accumulators][dscale nH][dq_bias 32 nH] floats
     assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
     assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4
+    # weight-gradient plan: one tile, 256 token chunks of [dW | db] partials
+    assert lib.hvk_weight_grad_supported(802816, 288, 96) == 1
+    assert lib.hvk_weight_grad_workspace(802816, 288, 96) == 256 * (288 * 96 + 288) * 4
+    assert lib.hvk_weight_grad_supported(802816 + 16, 288, 96) == 0  # M % 32
+    assert lib.hvk_weight_grad_supported(4096, 100, 96) == 0
 
 
 def test_library_rejects_bad_arguments_without_gpu():

@@ -12,6 +12,8 @@ SHAPES = [  # (name, M, N, K): dW [N, K] = g[M, N]^T x[M, K]
     ("s0.fc2", 802816, 96, 384), ("s1.qkv", 200704, 576, 192), ("s1.fc1", 200704, 768, 192),
     ("s1.fc2", 200704, 192, 768), ("s2.qkv", 50176, 1152, 384), ("s2.fc1", 50176, 1536, 384),
     ("s2.fc2", 50176, 384, 1536), ("s3.fc1", 12544, 3072, 768),
+    ("s1.proj", 200704, 192, 192), ("s2.proj", 50176, 384, 384), ("s3.qkv", 12544, 2304, 768),
+    ("s3.fc2", 12544, 768, 3072), ("s3.proj", 12544, 768, 768), ("merge1", 200704, 192, 384),
 ]
 
 
@@ -33,7 +35,7 @@ def main():
         g = torch.randn(M, N, device="cuda").bfloat16()
         x = torch.randn(M, K, device="cuda").bfloat16()
         line = [f"{name:8s} M={M:6d} N={N:4d} K={K:4d} bytes-bound {(M * (N + K) * 2) / 5e12 * 1e6:6.1f} us |"]
-        for nc in (1, 16, 32, 64, 128, 256):
+        for nc in ((1, 16, 64, 128) if os.environ.get("DW_ALL") else (64,)):
             if M % nc or M // nc < 64:
                 continue
             kc = M // nc
@@ -44,6 +46,13 @@ def main():
                 return torch.bmm(g.view(nc, kc, N).transpose(1, 2), x.view(nc, kc, K),
                                  out_dtype=torch.float32).sum(dim=0)
             line.append(f"nc{nc} {timeit(f):6.1f}")
+        from hvamd import ops
+        if ops._lib.load().hvk_weight_grad_supported(M, N, K):
+            line.append(f"| hvk {timeit(lambda: ops.weight_grad(g, x, False)):6.1f}"
+                        f" +db {timeit(lambda: ops.weight_grad(g, x, True)):6.1f}")
+            dw, _ = ops.weight_grad(g, x)
+            ref = torch.mm(g.t(), x, out_dtype=torch.float32)
+            line.append(f"err {((dw - ref).norm() / ref.norm()).item():.1e}")
         print(" ".join(line), flush=True)
         del g, x
 
