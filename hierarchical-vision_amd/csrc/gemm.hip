@@ -189,7 +189,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
         float v = cs[j][e];
 #pragma unroll
         for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m);
-        if (li == 0) atomicAdd(csum + n0 + 32 * j + 8 * g + e, v);
+        if (li == 0 && csum) atomicAdd(csum + n0 + 32 * j + 8 * g + e, v);
       }
   }
 }
@@ -330,7 +330,7 @@ int hvk_linear_gelu_bwd_supported(int M, int K, int N) {
 
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias,
                         int M, int K, int N, void* stream) {
-  if (!gy || !w || !h || !gh || !dbias)
+  if (!gy || !w || !h || !gh)
     return hvk_set_error(HVK_EINVAL, "hvk_linear_gelu_bwd: null pointer");
   if (!hvk_linear_gelu_bwd_supported(M, K, N))
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_gelu_bwd: shape M=%d K=%d N=%d not built", M, K, N);

@@ -161,6 +161,18 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     if (kt + 2 < KT) issue(kt + 2, kt & 1);
   }
 
+  // EPI 2: the 8 h vectors of this lane, loaded as one batch before the epilogue math
+  uint4 hp[EPI == 2 ? 4 : 1][2];
+  if (EPI == 2) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      int row = m0 + 64 * wm + 16 * b + li;
+      if (row >= M) row = M - 1;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + n0 + 64 * wn + 32 * j + 8 * g);
+    }
+  }
   // epilogue: lane (li, g) holds, for m-tile b and n-tile pair (2j, 2j+1), row
   // m0 + 64wm + 16b + li and columns n0 + 64wn + 32j + 8g .. +7
 #pragma unroll
@@ -176,11 +188,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
         v[r] = acc[2 * j][b][r];
         v[4 + r] = acc[2 * j + 1][b][r];
       }
-      if (bias) {
+      if (EPI != 2 && bias) {
         const float4 b0 = *reinterpret_cast<const float4*>(bias + col);
         const float4 b1 = *reinterpret_cast<const float4*>(bias + col + 4);
         v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
         v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      }
+      if (EPI == 2) {  // gh = (gy w) * GELU'(h): h (Y2) read in the output layout
+        float hf[8];
+        hvk_unpack8(hp[b][j], hf);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= hvk_gelu::gelu_grad(hf[e]);
+        *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hvk_pack8(v);
+        continue;
       }
       const uint4 hv = hvk_pack8(v);
       *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hv;
@@ -243,6 +263,17 @@ int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_fwd: M=%d K=%d N=%d (K %% 64, N %% 128)", M, K, N);
   return launch_tile<0>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
                         static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream));
+}
+
+int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, int M, int K, int N,
+                      void* stream) {
+  if (!gy || !w || !h || !gh) return hvk_set_error(HVK_EINVAL, "hvk_gemm_gelu_bwd: null pointer");
+  if (!hvk_gemm_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_gelu_bwd: M=%d K=%d N=%d", M, K, N);
+  return launch_tile<2>(static_cast<const hvk_bf16*>(gy), static_cast<const hvk_bf16*>(w), nullptr,
+                        static_cast<hvk_bf16*>(gh),
+                        const_cast<hvk_bf16*>(static_cast<const hvk_bf16*>(h)), M, N, K,
+                        static_cast<hipStream_t>(stream));
 }
 
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M, int K,

@@ -427,9 +427,10 @@ def linear_gelu(x, weight, bias):
 
 class MlpFn(torch.autograd.Function):
     """fc2(GELU(fc1(x))) (swinv2.py:58-65 with drop = 0): forward = the fused fc1 + GELU kernel
-    and the fc2 GEMM; backward runs fc2's input gradient with the activation backward and the
-    fc1 bias gradient in ONE kernel (hvk_linear_gelu_bwd) instead of GEMM -> bf16 dy1 ->
-    activation kernel.  fc2's bias, when given, is added by the GEMM (else folded downstream)."""
+    and the fc2 GEMM; backward runs fc2's input gradient and the activation backward as ONE
+    kernel (hvk_linear_gelu_bwd; the tiled hvk_gemm_gelu_bwd for stage 2) instead of GEMM ->
+    bf16 dy1 -> activation kernel, and the fc1 bias gradient rides on fc1's weight-gradient
+    kernel.  fc2's bias, when given, is added by the GEMM (else folded downstream)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
@@ -454,14 +455,17 @@ class MlpFn(torch.autograd.Function):
         M = g2.shape[0]
         dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
-        db1 = torch.zeros(N1, device=h.device, dtype=torch.float32)
-        call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2b.t().contiguous()), ptr(h), ptr(gh), ptr(db1),
-             M, N2, N1, stream())
+        w2t = w2b.t().contiguous()
+        if _tile_ok(M, N2, N1):
+            call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
+        else:
+            call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1,
+                 stream())
         gx = None
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, w1b.t().contiguous()) if _native_nt(M, N1, K)
                   else gh @ w1b).reshape(xb.shape)
-        dw1 = weight_grad(gh, xb.reshape(-1, K))[0]
+        dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
         return gx, dw1, db1, dw2, db2
 
 

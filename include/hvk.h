@@ -85,8 +85,8 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
 /* fc2 input gradient through the MLP activation (swinv2.py:58-65 backward): gh =
  * bf16((gy w^T) * GELU'(h)) with gy: bf16 [M, K] (gradient of fc2's output), w: bf16 [N, K]
  * (= fc2.weight^T), h: bf16 [M, N] (fc1's pre-activation saved by hvk_linear_gelu_fwd);
- * dbias: f32 [N], ACCUMULATED into (+= column sums of gh = the fc1 bias gradient; the caller
- * zeroes it).  Replaces the input-gradient GEMM + activation backward + bias reduction for
+ * dbias: f32 [N] or NULL, ACCUMULATED into (+= column sums of gh = the fc1 bias gradient;
+ * the caller zeroes it).  Replaces the input-gradient GEMM + activation backward + bias reduction for
  * the (K, N) shapes hvk_linear_gelu_bwd_supported() reports. */
 int hvk_linear_gelu_bwd_supported(int M, int K, int N);
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias, int M,
@@ -102,6 +102,11 @@ int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M
                  void* stream);
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                       int K, int N, void* stream);
+/* fc2 input gradient through the activation on the tiled kernel (the stage-2 form of
+ * hvk_linear_gelu_bwd, without the bias gradient): gh = bf16((gy w^T) * GELU'(h)), gy [M, K],
+ * w [N, K] (= fc2.weight^T), h [M, N] the saved pre-activation. */
+int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, int M, int K, int N,
+                      void* stream);
 
 /* ---- Weight-gradient GEMM (the backward of every SwinV2 Linear) ----------------------
  * dw[N, K] = g[M, N]^T x[M, K] in f32 and, when db is not NULL, db[N] = sum_m g[m, n]

@@ -144,3 +144,24 @@ def test_gemm_tile_gelu_matches_fp32():
     assert ((h.float() - href).norm() / href.norm()).item() < 1e-2
     yref = torch.nn.functional.gelu(h.float())
     assert ((y.float() - yref).norm() / yref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M", [50176, 1000])
+def test_gemm_tile_gelu_bwd_matches_fp32(M):
+    """fc2 input gradient through GELU' on the tiled kernel (hvk_gemm_gelu_bwd): gh =
+    (gy w2) * GELU'(h), against fp32 math on the same bf16 operands (ragged M included)."""
+    from hvamd import _lib
+    K, N = 384, 1536  # gy width (fc2 out), fc1 width
+    g = torch.Generator(device="cuda").manual_seed(11)
+    gy = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()  # fc2.weight^T
+    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    gh = torch.empty_like(h)
+    _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(gy), _lib.ptr(w), _lib.ptr(h), _lib.ptr(gh), M, K, N,
+              _lib.stream())
+    hf = h.float().requires_grad_(True)
+    torch.nn.functional.gelu(hf).backward(gy.float() @ w.float().t())
+    ref = hf.grad
+    torch.cuda.synchronize()
+    assert ((gh.float() - ref).norm() / ref.norm()).item() < 1e-2
+    assert (gh.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
