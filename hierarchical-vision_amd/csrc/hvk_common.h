@@ -126,10 +126,16 @@ __device__ __forceinline__ float erf_and_gauss(float x, float& e) {
   return copysignf(fmaf(-p, e, 1.f), x);
 }
 __device__ __forceinline__ float gelu(float u) {
+#ifdef HVK_PROBE_NOGELU
+  return u;
+#endif
   float e;
   return 0.5f * u * (1.f + erf_and_gauss(u * kInvSqrt2, e));
 }
 __device__ __forceinline__ float gelu_grad(float u) {
+#ifdef HVK_PROBE_NOGELU
+  return u;
+#endif
   float e;  // e = exp(-u^2/2)
   const float er = erf_and_gauss(u * kInvSqrt2, e);
   return fmaf(u * kInvSqrt2Pi, e, 0.5f * (1.f + er));
