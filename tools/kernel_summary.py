@@ -20,7 +20,8 @@ CATS = [  # (category, regex on the kernel name), first match wins
     ("bias_gelu", r"bias_gelu|colsum_rows"),
     ("patch_merge", r"merge_kernel"),
     ("losses", r"multitask|hxe"),
-    ("gemm(hvk)", r"linear_kernel|gemm_nt_kernel|gemm_tn"),
+    ("gemm(dW)", r"dw_kernel|dw_reduce"),
+    ("gemm(hvk)", r"linear_kernel|gemm_nt_kernel"),
     ("gemm", r"Cijk|gemm|Gemm|GEMM|mfma|MT\d+x\d+"),
     ("memset", r"[Mm]emset|fill"),
     ("reduce", r"reduce|Reduce"),
