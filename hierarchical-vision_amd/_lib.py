@@ -38,6 +38,7 @@ SIGNATURES = {
     "hvk_gemm_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_gelu_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_weight_grad_supported": (_i, [_i, _i, _i]),
+    "hvk_cast_weights": (_i, [_i, _p, _p, _p, _p, _p, _p]),
     "hvk_weight_grad_workspace": (_sz, [_i, _i, _i]),
     "hvk_weight_grad": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),

@@ -5,6 +5,7 @@ current stream; tensors are plumbing (PyTorch owns the memory).  There is no
 eager/CPU fallback: a CPU tensor or a missing library raises.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -37,6 +38,79 @@ def _bf16(t):
 def _f32(t):
     t = t if t.dtype == torch.float32 else t.float()
     return t.contiguous()
+
+
+# --------------------------------------------------------------------------- bf16 weights
+class _WeightCopies:
+    """bf16 copies (and transposes) of the f32 master weights, refreshed by ONE kernel per
+    step (`prepare_weights`, hvk_cast_weights) instead of a cast and a transpose per Linear
+    call.  A copy is served only while its master's version counter is unchanged, i.e. until
+    the optimizer updates the weight in place; otherwise the Linear casts on the fly."""
+
+    def __init__(self):
+        self.key = None
+        self.entries = {}
+        self.args = None
+        self.keep = []
+
+    def prepare(self, weights):
+        key = tuple((w.data_ptr(), tuple(w.shape)) for w in weights)
+        if key != self.key:
+            for w in weights:
+                if w.dtype != torch.float32 or w.dim() != 2 or not w.is_contiguous():
+                    raise RuntimeError("prepare_weights: contiguous 2-D f32 weights only")
+            self.entries, self.keep = {}, []
+            srcs, dsts, dts, rows, cols = [], [], [], [], []
+            for w in weights:
+                N, K = w.shape
+                wb = torch.empty((N, K), device=w.device, dtype=torch.bfloat16)
+                wt = torch.empty((K, N), device=w.device, dtype=torch.bfloat16)
+                self.keep += [wb, wt]
+                self.entries[(w.data_ptr(), (N, K))] = [wb, wt, -1]
+                srcs.append(ptr(w).value)
+                dsts.append(wb.data_ptr())
+                dts.append(wt.data_ptr())
+                rows.append(N)
+                cols.append(K)
+            n = len(weights)
+            arr = ctypes.c_void_p * n
+            self.arrays = (arr(*srcs), arr(*dsts), arr(*dts), (ctypes.c_int * n)(*rows),
+                           (ctypes.c_int * n)(*cols))
+            self.args = (n,) + tuple(ctypes.cast(a, ctypes.c_void_p) for a in self.arrays)
+            self.key = key
+        call("hvk_cast_weights", *self.args, stream())
+        for w in weights:
+            self.entries[(w.data_ptr(), tuple(w.shape))][2] = w._version
+
+    def get(self, w):
+        e = self.entries.get((w.data_ptr(), tuple(w.shape)))
+        if e is not None and e[2] == w._version and w.dtype == torch.float32:
+            return e[0], e[1]
+        return None
+
+
+_WCOPIES = _WeightCopies()
+_PREPARE = os.environ.get("HVK_PREPARE_WEIGHTS", "1") != "0"  # 0: per-call casts (A/B runs)
+
+
+def prepare_weights(weights):
+    """Refresh the bf16 copies (+ transposes) of `weights` (f32 [N, K] masters) in one launch;
+    the Linear Functions below then use them for this step."""
+    if weights and _PREPARE:
+        _WCOPIES.prepare(weights)
+
+
+def _bf16_weight(w):
+    """(bf16 W, bf16 W^T or None) for a Linear weight: the step's prepared copies when they
+    are current, else a cast now (the transpose is then made where needed)."""
+    c = _WCOPIES.get(w)
+    if c is not None:
+        return c
+    return w.to(torch.bfloat16), None
+
+
+def _bf16_t(wb, wt):
+    return wt if wt is not None else wb.t().contiguous()
 
 
 # --------------------------------------------------------------------------- Linear
@@ -150,10 +224,11 @@ class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         xb = _bf16(x)
-        wb = weight.to(torch.bfloat16)
+        wb, wt = _bf16_weight(weight)
         N, K = wb.shape
         y = mm_nt(xb.reshape(-1, K), wb, bias).reshape(*xb.shape[:-1], N)
         ctx.save_for_backward(xb, wb)
+        ctx.wt = wt
         ctx.has_bias = bias is not None
         return y
 
@@ -164,7 +239,7 @@ class LinearFn(torch.autograd.Function):
         g2 = _bf16(gy).reshape(-1, N)
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(g2, wb.t().contiguous()) if _native_nt(g2.shape[0], N, K)
+            gx = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K)
                   else g2 @ wb).reshape(xb.shape)
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = None, None
@@ -389,10 +464,11 @@ class LinearGelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         xb = _bf16(x)
-        wb = weight.to(torch.bfloat16)
+        wb, wt = _bf16_weight(weight)
         N, K = wb.shape
         h, y = gelu_fwd(xb.reshape(-1, K), wb, bias)
         ctx.save_for_backward(xb, wb, h)
+        ctx.wt = wt
         return y.reshape(*xb.shape[:-1], N)
 
     @staticmethod
@@ -409,7 +485,7 @@ class LinearGelu(torch.autograd.Function):
              stream())
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(gh, wb.t().contiguous()) if _native_nt(M, N, K)
+            gx = (mm_nt(gh, _bf16_t(wb, ctx.wt)) if _native_nt(M, N, K)
                   else gh @ wb).reshape(xb.shape)
         dw = weight_grad(gh, xb.reshape(-1, K))[0] if ctx.needs_input_grad[1] else None
         return gx, dw, db
@@ -435,8 +511,9 @@ class MlpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
         xb = _bf16(x)
-        w1b = w1.to(torch.bfloat16)
-        w2b = w2.to(torch.bfloat16)
+        w1b, w1t = _bf16_weight(w1)
+        w2b, w2t = _bf16_weight(w2)
+        ctx.wts = (w1t, w2t)
         N1, K = w1b.shape
         x2 = xb.reshape(-1, K)
         M = x2.shape[0]
@@ -455,7 +532,7 @@ class MlpFn(torch.autograd.Function):
         M = g2.shape[0]
         dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
-        w2t = w2b.t().contiguous()
+        w2t = _bf16_t(w2b, ctx.wts[1])
         if _tile_ok(M, N2, N1):
             call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
         else:
@@ -463,7 +540,7 @@ class MlpFn(torch.autograd.Function):
                  stream())
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = (mm_nt(gh, w1b.t().contiguous()) if _native_nt(M, N1, K)
+            gx = (mm_nt(gh, _bf16_t(w1b, ctx.wts[0])) if _native_nt(M, N1, K)
                   else gh @ w1b).reshape(xb.shape)
         dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
         return gx, dw1, db1, dw2, db2

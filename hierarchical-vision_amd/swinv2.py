@@ -532,7 +532,22 @@ class SwinTransformerV2(nn.Module):
         for i, blk in enumerate(blocks):
             blk._dp = None if probs[i] <= 0.0 else (scales[2 * i], scales[2 * i + 1])
 
+    def _gemm_weights(self):
+        """The f32 master weights every GEMM of a forward casts to bf16 (patch embed, qkv,
+        proj, fc1, fc2, reductions), refreshed together by ops.prepare_weights."""
+        ws = [self.patch_embed.proj.weight.reshape(self.patch_embed.embed_dim, -1)]
+        for m in self.modules():
+            if isinstance(m, WindowAttention):
+                ws += [m.qkv.weight, m.proj.weight]
+            elif isinstance(m, Mlp):
+                ws += [m.fc1.weight, m.fc2.weight]
+            elif isinstance(m, PatchMerging):
+                ws.append(m.reduction.weight)
+        return [w for w in ws if w.dtype == torch.float32 and w.is_contiguous()]
+
     def forward_features(self, x, output_activations=False):
+        if x.is_cuda:  # one launch for all bf16 weight copies of this step
+            ops.prepare_weights(self._gemm_weights())
         self._plan_drop_path(x.shape[0], x.device)
         s = self.patch_embed.forward_stream(x)
         if self.ape:

@@ -120,6 +120,14 @@ size_t hvk_weight_grad_workspace(int M, int N, int K);
 int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
                     void* ws, size_t ws_bytes, void* stream);
 
+/* ---- bf16 weight copies for a step --------------------------------------------------
+ * For k < n: dst[k] = bf16(src[k]) ([rows[k], cols[k]] row-major, f32 -> bf16 round to
+ * nearest even, as weight.to(torch.bfloat16)) and, when dst_t is not NULL and dst_t[k] is
+ * not NULL, dst_t[k] = its transpose [cols[k], rows[k]].  All weights in one launch per 64
+ * (the per-call casts of every autocast F.linear, swinv2.py:58-62, 220, 262, 296, 492). */
+int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* const* dst_t,
+                     const int* rows, const int* cols, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

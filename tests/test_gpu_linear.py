@@ -165,3 +165,46 @@ def test_gemm_tile_gelu_bwd_matches_fp32(M):
     torch.cuda.synchronize()
     assert ((gh.float() - ref).norm() / ref.norm()).item() < 1e-2
     assert (gh.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
+
+
+def test_cast_weights_bit_exact_and_transposed():
+    """hvk_cast_weights == weight.to(bfloat16) (round to nearest even) and its transpose, for
+    ragged shapes (not multiples of the 32 x 32 tile) in one launch."""
+    import ctypes
+    from hvamd import _lib
+    shapes = [(288, 96), (96, 96), (33, 70), (1, 5), (768, 3072), (10, 1)]
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    ws = [torch.randn(s, device="cuda", generator=gen) * 3 for s in shapes]
+    dst = [torch.empty(s, device="cuda", dtype=torch.bfloat16) for s in shapes]
+    dtt = [torch.empty(s[::-1], device="cuda", dtype=torch.bfloat16) for s in shapes]
+    n = len(shapes)
+    arr = ctypes.c_void_p * n
+    a = [arr(*[t.data_ptr() for t in ts]) for ts in (ws, dst, dtt)]
+    rows = (ctypes.c_int * n)(*[s[0] for s in shapes])
+    cols = (ctypes.c_int * n)(*[s[1] for s in shapes])
+    _lib.call("hvk_cast_weights", n, *[ctypes.cast(x, ctypes.c_void_p) for x in a],
+              ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cols, ctypes.c_void_p), _lib.stream())
+    torch.cuda.synchronize()
+    for w, d, t in zip(ws, dst, dtt):
+        assert torch.equal(d, w.to(torch.bfloat16))
+        assert torch.equal(t, w.to(torch.bfloat16).t())
+
+
+def test_prepared_weights_follow_in_place_updates():
+    """The step's bf16 copies are used while the master is unchanged and bypassed after an
+    in-place (optimizer-style) update until the next prepare."""
+    from hvamd import ops
+    torch.manual_seed(1)
+    w = torch.randn(288, 96, device="cuda")
+    x = torch.randn(4096, 96, device="cuda").bfloat16()
+    ops.prepare_weights([w])
+    wb, wt = ops._bf16_weight(w)
+    assert torch.equal(wb, w.bfloat16()) and torch.equal(wt, w.bfloat16().t())
+    y0 = ops.linear(x, w)
+    with torch.no_grad():
+        w.mul_(2.0)  # version bump: the prepared copy is stale now
+    y1 = ops.linear(x, w)
+    torch.cuda.synchronize()
+    assert torch.allclose(y1.float(), 2 * y0.float(), rtol=2e-2, atol=1e-2)
+    ops.prepare_weights([w])
+    assert torch.equal(ops._bf16_weight(w)[0], w.bfloat16())

@@ -15,7 +15,10 @@ STAGES = [(802816, 96), (200704, 192), (50176, 384)]
 def main():
     from hvamd import _lib
     P, st = _lib.ptr, _lib.stream
-    for M, C in STAGES:
+    stages = STAGES
+    if len(sys.argv) > 1:  # python tools/bench_mlp.py 0  -> stage 0 only
+        stages = [STAGES[int(a)] for a in sys.argv[1:]]
+    for M, C in stages:
         N = 4 * C
         x = torch.randn(M, C, device="cuda").bfloat16()
         w1 = (torch.randn(N, C, device="cuda") / C ** 0.5).bfloat16()
