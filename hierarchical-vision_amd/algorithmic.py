@@ -104,6 +104,15 @@ class GradientClipping(Algorithm):
 
     def apply(self, event, state, logger=None):
         params = [p for p in state.model.parameters() if p.grad is not None]
+        opts = getattr(state, "optimizers", None) or []
+        opt = opts[0] if len(opts) == 1 else None
+        if (self.clipping_type == "norm" and opt is not None
+                and getattr(opt, "supports_fused_clip", lambda: False)()
+                and {id(p) for p in params} <= {id(q) for g in opt.param_groups for q in g["params"]}):
+            # the optimizer's step applies the clip coefficient on the fly (same global norm,
+            # computed on the device in the fused update, no host synchronisation)
+            opt.pending_clip = self.clipping_threshold
+            return
         if self.clipping_type == "norm":
             torch.nn.utils.clip_grad_norm_(params, self.clipping_threshold, foreach=True)
         else:

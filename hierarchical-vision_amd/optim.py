@@ -4,6 +4,8 @@ no-decay rule and multi-tensor (foreach) update kernels.
 Quirk kept from the reference: build_optimizer is handed the Composer wrapper,
 which has no `no_weight_decay`, so the skip set is always empty and 3-D
 `logit_scale` is decayed (optim.py:9-14, 53)."""
+import os
+
 import torch
 
 
@@ -29,9 +31,81 @@ class DecoupledSGDW(torch.optim.Optimizer):
                         nesterov=nesterov, initial_lr=lr)
         super().__init__(params, defaults)
 
+        self.pending_clip = None  # global-norm threshold handed over by GradientClipping
+        self._fused = None
+
+    def supports_fused_clip(self):
+        return True
+
+    def _fused_eligible(self):
+        if os.environ.get("HVK_FUSED_OPTIM", "1") == "0":  # A/B runs: the foreach path
+            return False
+        gs = self.param_groups
+        if not gs or any(g["nesterov"] != gs[0]["nesterov"] or g["momentum"] != gs[0]["momentum"]
+                         or g["dampening"] != gs[0]["dampening"] for g in gs):
+            return False
+        for g in gs:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if not (p.is_cuda and p.dtype == torch.float32 and p.grad.dtype == torch.float32
+                        and p.is_contiguous() and p.grad.is_contiguous()):
+                    return False
+        return gs[0]["momentum"] != 0 and len(gs) <= 4
+
+    def _fused_step(self):
+        """Clip + update of every tensor in a handful of libhvk launches (hvk_sgdw_step);
+        False (nothing done) when only some momentum buffers exist yet."""
+        import ctypes
+        from . import _lib
+        ps, grp = [], []
+        for gi, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                if p.grad is not None:
+                    ps.append(p)
+                    grp.append(gi)
+        if not ps:
+            return True
+        fresh = ["momentum_buffer" not in self.state[p] for p in ps]
+        if any(fresh) and not all(fresh):
+            return False
+        first = all(fresh)
+        if first:  # torch SGD semantics: the first step's buffer is the (clipped) gradient
+            for p in ps:
+                self.state[p]["momentum_buffer"] = torch.empty_like(p)
+        n = len(ps)
+        P = ctypes.c_void_p * n
+        numel = (ctypes.c_longlong * n)(*[p.numel() for p in ps])
+        arrs = (P(*[p.data_ptr() for p in ps]), P(*[p.grad.data_ptr() for p in ps]),
+                P(*[self.state[p]["momentum_buffer"].data_ptr() for p in ps]), numel,
+                (ctypes.c_int * n)(*grp))
+        gs = self.param_groups
+        lr = (ctypes.c_float * len(gs))(*[g["lr"] for g in gs])
+        decay = (ctypes.c_float * len(gs))(
+            *[1.0 - g["weight_decay"] * g["lr"] / g["initial_lr"] if g["weight_decay"] else 1.0
+              for g in gs])
+        lib = _lib.load()
+        nb = lib.hvk_sgdw_workspace_bytes(n, ctypes.cast(numel, ctypes.c_void_p))
+        if self._fused is None or self._fused.numel() * 4 < nb:
+            self._fused = torch.empty(nb // 4, device=ps[0].device, dtype=torch.float32)
+        clip = float(self.pending_clip) if self.pending_clip is not None else 0.0
+        g0 = gs[0]
+        _lib.call("hvk_sgdw_step", n, *[ctypes.cast(a, ctypes.c_void_p) for a in arrs],
+                  ctypes.cast(lr, ctypes.c_void_p), ctypes.cast(decay, ctypes.c_void_p), len(gs),
+                  clip, float(g0["momentum"]), float(g0["dampening"]), int(bool(g0["nesterov"])),
+                  int(first), _lib.ptr(self._fused), nb, _lib.stream())
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self._fused_eligible() and self._fused_step():
+            self.pending_clip = None
+            return loss
+        if self.pending_clip is not None:  # unfused: clip now, as GradientClipping would
+            params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+            torch.nn.utils.clip_grad_norm_(params, self.pending_clip, foreach=True)
+            self.pending_clip = None
         for g in self.param_groups:
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:

@@ -128,6 +128,20 @@ int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, i
 int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* const* dst_t,
                      const int* rows, const int* cols, void* stream);
 
+/* ---- Fused optimizer step (gradient-norm clipping + DecoupledSGDW) --------------------
+ * For the n f32 tensors p[k] (params), g[k] (grads), m[k] (momentum buffers) of numel[k]
+ * elements in parameter group group[k] < ngroups <= 4: with coef = min(1, max_norm /
+ * (||g||_2 + 1e-6)) over ALL n gradients (max_norm <= 0: coef = 1; torch clip_grad_norm_),
+ * g' = coef g, m = first ? g' : momentum m + (1 - dampening) g', u = nesterov ? g' +
+ * momentum m : m, p = p decay[group] - lr[group] u (composer DecoupledSGDW: decay =
+ * 1 - weight_decay lr / initial_lr).  g is not modified.  workspace: f32,
+ * hvk_sgdw_workspace_bytes(n, numel) bytes. */
+size_t hvk_sgdw_workspace_bytes(int n, const long long* numel);
+int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m,
+                  const long long* numel, const int* group, const float* lr, const float* decay,
+                  int ngroups, float max_norm, float momentum, float dampening, int nesterov,
+                  int first, float* workspace, size_t ws_bytes, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

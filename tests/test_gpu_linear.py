@@ -208,3 +208,29 @@ def test_prepared_weights_follow_in_place_updates():
     assert torch.allclose(y1.float(), 2 * y0.float(), rtol=2e-2, atol=1e-2)
     ops.prepare_weights([w])
     assert torch.equal(ops._bf16_weight(w)[0], w.bfloat16())
+
+
+def test_fused_sgdw_step_matches_foreach_path():
+    """hvk_sgdw_step (clip + DecoupledSGDW, one fused pass) against the foreach path of the same
+    optimizer on CPU copies: two steps (first-step buffer init, then the momentum update),
+    decay and no-decay groups, clipping active."""
+    from hvamd.optim import DecoupledSGDW
+    torch.manual_seed(0)
+    shapes = [(288, 96), (96,), (3, 1, 1), (70001,)]
+    ps_gpu = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in shapes]
+    ps_cpu = [torch.nn.Parameter(p.detach().cpu().clone()) for p in ps_gpu]
+
+    def groups(ps):
+        return [{"params": [ps[0], ps[2]]}, {"params": [ps[1], ps[3]], "weight_decay": 0.0}]
+    og = DecoupledSGDW(groups(ps_gpu), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    oc = DecoupledSGDW(groups(ps_cpu), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    for step in range(2):
+        for pg, pc in zip(ps_gpu, ps_cpu):
+            g = torch.randn(pg.shape) * 3
+            pg.grad, pc.grad = g.cuda(), g.clone()
+        og.pending_clip = 2.0
+        og.step()
+        torch.nn.utils.clip_grad_norm_(ps_cpu, 2.0)
+        oc.step()
+        for pg, pc in zip(ps_gpu, ps_cpu):
+            assert torch.allclose(pg.detach().cpu(), pc.detach(), rtol=1e-5, atol=1e-6), step

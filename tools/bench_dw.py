@@ -31,7 +31,10 @@ def timeit(fn, iters=20):
 
 
 def main():
+    only = set(sys.argv[1:])  # e.g. python tools/bench_dw.py s2.qkv
     for name, M, N, K in SHAPES:
+        if only and name not in only:
+            continue
         g = torch.randn(M, N, device="cuda").bfloat16()
         x = torch.randn(M, K, device="cuda").bfloat16()
         line = [f"{name:8s} M={M:6d} N={N:4d} K={K:4d} bytes-bound {(M * (N + K) * 2) / 5e12 * 1e6:6.1f} us |"]
