@@ -12,7 +12,7 @@
 namespace {
 
 constexpr int kHid = 512;  // cpb_mlp hidden width (swinv2.py:141)
-constexpr int kRowsPerBlock = 16;
+constexpr int kRowsPerBlock = 8;  // 22 workgroups for the (2w-1)^2 = 169 rows of w7
 
 // one wave per (h, r) output: lane l owns hidden units l, l+64, ... (8 of 512), the dot
 // product is a wave reduction; the hidden layer is recomputed per head (<= 32 heads, tiny)
@@ -64,9 +64,12 @@ __global__ __launch_bounds__(kHid) void cpb_bwd_partial_kernel(
   }
   __syncthreads();
   const float w10 = w1[2 * j], w11 = w1[2 * j + 1], bj = b1[j];
-  float dw2[32];
+  float dw2[32], w2j[32];  // this hidden unit's W2 column, loaded once (all loads in flight)
 #pragma unroll
-  for (int h = 0; h < 32; ++h) dw2[h] = 0.f;
+  for (int h = 0; h < 32; ++h) {
+    dw2[h] = 0.f;
+    w2j[h] = h < nH ? w2[(size_t)h * kHid + j] : 0.f;
+  }
   float dw10 = 0.f, dw11 = 0.f, db = 0.f;
   for (int rr = 0; rr < kRowsPerBlock; ++rr) {
     const int r = r0 + rr;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(kHid) void cpb_bwd_partial_kernel(
       if (h < nH) {
         const float d = dpre[rr][h];
         dw2[h] = fmaf(d, a, dw2[h]);
-        dh = fmaf(d, w2[(size_t)h * kHid + j], dh);
+        dh = fmaf(d, w2j[h], dh);
       }
     }
     dh = hid > 0.f ? dh : 0.f;
