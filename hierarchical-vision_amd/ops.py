@@ -254,6 +254,45 @@ def linear(x, weight, bias=None):
     return LinearFn.apply(x, weight, bias)
 
 
+# --------------------------------------------------------------------------- block biases
+class AttnBiasFn(torch.autograd.Function):
+    """(qkv GEMM bias (q_bias, 0, 0), proj bias + W_proj v_bias) of a W-MSA block in ONE
+    launch (hvk_attn_bias_fwd) and its backward in one more, instead of zeros + cat + a
+    GEMV + an add forward and the matching autograd chain backward (swinv2.py:218-220, 262).
+    q_bias enters detached: its gradient is the W-MSA backward's column sums of dq."""
+
+    @staticmethod
+    def forward(ctx, v_bias, proj_bias, proj_w, q_bias):
+        C = v_bias.numel()
+        v, w = _f32(v_bias), _f32(proj_w)
+        pb = _f32(proj_bias) if proj_bias is not None else None
+        qb = _f32(q_bias.detach()) if q_bias is not None else None
+        qkv_bias = torch.empty(3 * C, device=v.device, dtype=torch.float32)
+        eff = torch.empty(C, device=v.device, dtype=torch.float32)
+        call("hvk_attn_bias_fwd", ptr(qb), ptr(v), ptr(pb), ptr(w), C, ptr(qkv_bias), ptr(eff),
+             stream())
+        ctx.save_for_backward(v, w)
+        ctx.has_pb = proj_bias is not None
+        ctx.mark_non_differentiable(qkv_bias)
+        return qkv_bias, eff
+
+    @staticmethod
+    def backward(ctx, g_qkv, g_eff):
+        v, w = ctx.saved_tensors
+        if g_eff is None:
+            return None, None, None, None
+        g = _f32(g_eff)
+        C = v.numel()
+        dpb = torch.empty_like(g) if ctx.has_pb else None
+        dv, dw = torch.empty_like(v), torch.empty_like(w)
+        call("hvk_attn_bias_bwd", ptr(g), ptr(v), ptr(w), C, ptr(dpb), ptr(dv), ptr(dw), stream())
+        return dv, dpb, dw, None
+
+
+def attn_biases(q_bias, v_bias, proj_bias, proj_w):
+    return AttnBiasFn.apply(v_bias, proj_bias, proj_w, q_bias)
+
+
 # --------------------------------------------------------------------------- W-MSA
 _WMSA_WS = {}
 

@@ -213,15 +213,23 @@ class WindowAttention(nn.Module):
         with torch.autocast(device_type=self.v_bias.device.type, enabled=False):
             return self.proj.bias + F.linear(self.v_bias.float(), self.proj.weight.float())
 
-    def forward_tokens(self, x, H, W, shift, proj_bias=True):
+    def gemm_biases(self):
+        """(qkv GEMM bias, proj bias) = (qkv_gemm_bias(), proj_bias()), on the GPU as one
+        fused launch (ops.attn_biases)."""
+        if self.v_bias is not None and self.v_bias.is_cuda:
+            return ops.attn_biases(self.q_bias, self.v_bias, self.proj.bias, self.proj.weight)
+        return self.qkv_gemm_bias(), self.proj_bias()
+
+    def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None):
         """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] after proj (without
-        proj's bias when proj_bias=False: the caller folds self.proj_bias() into the next
-        kernel)."""
-        qkv = ops.linear(x, self.qkv.weight, self.qkv_gemm_bias())
+        proj's bias when proj_bias=False: the caller folds the proj bias into the next
+        kernel).  biases: gemm_biases() when the caller already has them."""
+        qkv_b, proj_b = biases if biases is not None else self.gemm_biases()
+        qkv = ops.linear(x, self.qkv.weight, qkv_b)
         table, scale = self.cpb_tables()
         o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
                                       self.window_size[0], shift, q_bias=self.q_bias)
-        return self.proj_drop(ops.linear(o, self.proj.weight, self.proj_bias() if proj_bias else None))
+        return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -291,13 +299,15 @@ class SwinTransformerBlock(nn.Module):
         B, L, C = s.f32.shape
         assert L == H * W, "input feature has wrong size"
         fold = self.attn.proj_drop.p == 0 or not self.training  # proj bias -> LN kernel
-        a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold)
+        biases = self.attn.gemm_biases()
+        a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold,
+                                     biases=biases)
         planned = getattr(self, "_dp", None) if self.training else None  # from _plan_drop_path
         if planned is not None and planned[0].shape[0] != B:
             planned = None
         dp = planned[0] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
         x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
-                                        self.norm1.eps, abias=self.attn.proj_bias() if fold else None)
+                                        self.norm1.eps, abias=biases[1] if fold else None)
         fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
         h = self.mlp.forward_tokens(xb, fc2_bias=not fold)
         dp = planned[1] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)

@@ -142,6 +142,16 @@ int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m
                   int ngroups, float max_norm, float momentum, float dampening, int nesterov,
                   int first, float* workspace, size_t ws_bytes, void* stream);
 
+/* ---- W-MSA block biases (swinv2.py:218-220, 262) --------------------------------------
+ * Forward: qkv_bias[3C] = (q_bias or 0, 0, 0) and eff[C] = proj_bias (or 0) + proj_w v_bias
+ * (proj_w f32 [C, C]): the qkv GEMM's bias and proj's bias with v_bias folded in (softmax
+ * rows sum to 1, so P (V + v_bias) = P V + v_bias).  Backward of eff w.r.t. g = d eff:
+ * d_proj_bias = g (if not NULL), d_v_bias = proj_w^T g, d_proj_w = g v_bias^T (written). */
+int hvk_attn_bias_fwd(const float* q_bias, const float* v_bias, const float* proj_bias,
+                      const float* proj_w, int C, float* qkv_bias, float* eff, void* stream);
+int hvk_attn_bias_bwd(const float* g, const float* v_bias, const float* proj_w, int C,
+                      float* d_proj_bias, float* d_v_bias, float* d_proj_w, void* stream);
+
 /* ---- Continuous relative-position bias table + logit scale (one block) ---------------
  * table[h, r] = 16 sigmoid(w2[h, :] . relu(w1 coords[r, :] + b1)), scale[h] =
  * exp(min(logit_scale[h], clamp_max)): swinv2.py:141-145 (cpb_mlp), 233-246 (16 sigmoid,

@@ -234,3 +234,25 @@ def test_fused_sgdw_step_matches_foreach_path():
         oc.step()
         for pg, pc in zip(ps_gpu, ps_cpu):
             assert torch.allclose(pg.detach().cpu(), pc.detach(), rtol=1e-5, atol=1e-6), step
+
+
+@pytest.mark.parametrize("C", [96, 768])
+def test_attn_biases_match_torch(C):
+    """hvk_attn_bias_fwd/bwd: (q_bias, 0, 0) and proj.bias + W v_bias with their gradients
+    against the torch ops they replace (swinv2.py:218-220, 262 folding)."""
+    from hvamd import ops
+    torch.manual_seed(C)
+    qb = torch.randn(C, device="cuda", requires_grad=True)
+    vb = torch.randn(C, device="cuda", requires_grad=True)
+    pb = torch.randn(C, device="cuda", requires_grad=True)
+    w = torch.randn(C, C, device="cuda", requires_grad=True)
+    qkv_b, eff = ops.attn_biases(qb, vb, pb, w)
+    g = torch.randn(C, device="cuda")
+    eff.backward(g)
+    ref_eff = pb.detach() + w.detach() @ vb.detach()
+    assert torch.equal(qkv_b[:C], qb.detach()) and not qkv_b[C:].any()
+    assert torch.allclose(eff, ref_eff, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(vb.grad, w.detach().t() @ g, rtol=1e-5, atol=1e-4)
+    assert torch.equal(pb.grad, g)
+    assert torch.allclose(w.grad, torch.outer(g, vb.detach()), rtol=1e-6, atol=1e-6)
+    assert qb.grad is None
