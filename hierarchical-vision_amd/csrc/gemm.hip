@@ -145,7 +145,11 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           float hv[8];
           hvk_unpack8(hf[EPI == 2 ? j : 0], hv);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= hvk_gelu::gelu_grad(hv[e]);
+          for (int e = 0; e < 8; e += 2) {
+            const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hv[e], hv[e + 1]});
+            v[e] *= d.x;
+            v[e + 1] *= d.y;
+          }
           const uint4 gv = hvk_pack8(v);
           hvk_st16(yp + 32 * j, gv);
           float r[8];
@@ -166,7 +170,11 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           float u[8];
           hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
 #pragma unroll
-          for (int e = 0; e < 8; ++e) u[e] = hvk_gelu::gelu(u[e]);
+          for (int e = 0; e < 8; e += 2) {
+            const hvk_gelu::f32x2 y = hvk_gelu::gelu2(hvk_gelu::f32x2{u[e], u[e + 1]});
+            u[e] = y.x;
+            u[e + 1] = y.y;
+          }
           hvk_st16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j, hvk_pack8(u));
         }
       }

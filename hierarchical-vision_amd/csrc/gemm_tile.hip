@@ -198,7 +198,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
         float hf[8];
         hvk_unpack8(hp[b][j], hf);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] *= hvk_gelu::gelu_grad(hf[e]);
+        for (int e = 0; e < 8; e += 2) {
+          const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hf[e], hf[e + 1]});
+          v[e] *= d.x;
+          v[e + 1] *= d.y;
+        }
         *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hvk_pack8(v);
         continue;
       }
@@ -208,7 +212,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
         float u[8];
         hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
 #pragma unroll
-        for (int e = 0; e < 8; ++e) u[e] = hvk_gelu::gelu(u[e]);
+        for (int e = 0; e < 8; e += 2) {
+            const hvk_gelu::f32x2 y = hvk_gelu::gelu2(hvk_gelu::f32x2{u[e], u[e + 1]});
+            u[e] = y.x;
+            u[e + 1] = y.y;
+          }
         *reinterpret_cast<uint4*>(Y2 + (size_t)row * N + col) = hvk_pack8(u);
       }
     }

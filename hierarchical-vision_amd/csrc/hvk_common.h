@@ -140,6 +140,38 @@ __device__ __forceinline__ float gelu_grad(float u) {
   const float er = erf_and_gauss(u * kInvSqrt2, e);
   return fmaf(u * kInvSqrt2Pi, e, 0.5f * (1.f + er));
 }
+// The same functions on pairs: the polynomial and products as packed f32 (v_pk_fma_f32 /
+// v_pk_mul_f32), the same operations and rounding per element as the scalar forms above.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 erf_and_gauss2(f32x2 x, f32x2& e) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 d = ax * 0.3275911f + 1.f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f + -1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t + -0.284496736f;
+  p = p * t + 0.254829592f;
+  p = p * t;
+  const f32x2 q = -ax * ax * 1.4426950408889634f;
+  e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 r = -p * e + 1.f;
+  return f32x2{copysignf(r.x, x.x), copysignf(r.y, x.y)};
+}
+__device__ __forceinline__ f32x2 gelu2(f32x2 u) {
+#ifdef HVK_PROBE_NOGELU
+  return u;
+#endif
+  f32x2 e;
+  return 0.5f * u * (1.f + erf_and_gauss2(u * kInvSqrt2, e));
+}
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 u) {
+#ifdef HVK_PROBE_NOGELU
+  return u;
+#endif
+  f32x2 e;
+  const f32x2 er = erf_and_gauss2(u * kInvSqrt2, e);
+  return (u * kInvSqrt2Pi) * e + 0.5f * (1.f + er);
+}
 }  // namespace hvk_gelu
 
 // ---- MFMA 16x16x32 bf16 -> f32 --------------------------------------------

@@ -12,8 +12,6 @@
 namespace {
 
 constexpr int kWaves = 4;
-using hvk_gelu::gelu;
-using hvk_gelu::gelu_grad;
 
 
 __global__ __launch_bounds__(64 * kWaves) void bias_gelu_fwd_kernel(const hvk_bf16* __restrict__ h,
@@ -31,7 +29,11 @@ __global__ __launch_bounds__(64 * kWaves) void bias_gelu_fwd_kernel(const hvk_bf
     float f[8];
     hvk_unpack8(*reinterpret_cast<const uint4*>(h + off), f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = gelu(f[j] + bb[j]);
+    for (int j = 0; j < 8; j += 2) {
+      const hvk_gelu::f32x2 v = hvk_gelu::gelu2(hvk_gelu::f32x2{f[j] + bb[j], f[j + 1] + bb[j + 1]});
+      f[j] = v.x;
+      f[j + 1] = v.y;
+    }
     *reinterpret_cast<uint4*>(y + off) = hvk_pack8(f);
   }
 }
@@ -60,9 +62,12 @@ __global__ __launch_bounds__(64 * kWaves) void bias_gelu_bwd_kernel(const hvk_bf
       hvk_unpack8(*reinterpret_cast<const uint4*>(h + off), u);
       hvk_unpack8(*reinterpret_cast<const uint4*>(gy + off), g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        g[j] *= gelu_grad(u[j] + bb[j]);
+      for (int j = 0; j < 8; j += 2) {
+        const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{u[j] + bb[j], u[j + 1] + bb[j + 1]});
+        g[j] *= d.x;
+        g[j + 1] *= d.y;
         acc[j] += g[j];
+        acc[j + 1] += g[j + 1];
       }
       *reinterpret_cast<uint4*>(gh + off) = hvk_pack8(g);
     }

@@ -50,7 +50,6 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
   const int h = grp * HG + wave;
   const int per_img = g.nWh * g.nWw;
   const char* qkv = reinterpret_cast<const char*>(a.qkv);
-  const size_t row_bytes = (size_t)6 * C;
   const int grp_off = grp * HG * 64;  // byte offset of the group inside a q/k/v part
 
   char* zero16 = smem + K::SLAB;
@@ -164,7 +163,6 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
       if (ky >= WIN - g.shift) kband |= 1u << (ki * 4 + r);
       if (kx >= WIN - g.shift) kband |= 1u << (16 + ki * 4 + r);
     }
-  const int hs = wave * 4 + gq;  // this lane's 16-B slot inside a part of a token
 
   // window coordinates advance incrementally (no per-window integer divisions)
   int cb = w0 / per_img, cwh = (w0 % per_img) / g.nWw, cww = w0 % g.nWw;
