@@ -14,9 +14,12 @@ __global__ __launch_bounds__(256) void attn_bias_fwd_kernel(const float* __restr
                                                             const float* __restrict__ pb,
                                                             const float* __restrict__ w, int C,
                                                             float* __restrict__ qkv_bias,
-                                                            float* __restrict__ eff) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < 3 * C; i += gridDim.x * 256)
+                                                            float* __restrict__ eff,
+                                                            float* __restrict__ dv_zero) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 3 * C; i += gridDim.x * 256) {
     qkv_bias[i] = (i < C && qb) ? qb[i] : 0.f;
+    if (dv_zero && i < C) dv_zero[i] = 0.f;  // the backward's d v_bias accumulator
+  }
   // one wave per output row n: lanes stride over k, wave reduction
   const int lane = threadIdx.x & 63;
   for (int n = blockIdx.x * 4 + (threadIdx.x >> 6); n < C; n += gridDim.x * 4) {
@@ -28,7 +31,8 @@ __global__ __launch_bounds__(256) void attn_bias_fwd_kernel(const float* __restr
 }
 
 // 8 rows n of W per workgroup: d W[n, :] = g[n] v^T and the rows' share of d v = W^T g
-// (column partial sums, one f32 atomic per column per workgroup; d v zeroed by the caller)
+// (column partial sums, one f32 atomic per column per workgroup into d v, which the
+// forward launch zeroed)
 constexpr int kRows = 8;
 __global__ __launch_bounds__(256) void attn_bias_bwd_kernel(const float* __restrict__ g,
                                                             const float* __restrict__ vb,
@@ -60,12 +64,13 @@ __global__ __launch_bounds__(256) void attn_bias_bwd_kernel(const float* __restr
 extern "C" {
 
 int hvk_attn_bias_fwd(const float* q_bias, const float* v_bias, const float* proj_bias,
-                      const float* proj_w, int C, float* qkv_bias, float* eff, void* stream) {
+                      const float* proj_w, int C, float* qkv_bias, float* eff, float* dv_zero,
+                      void* stream) {
   if (!v_bias || !proj_w || !qkv_bias || !eff || C <= 0)
     return hvk_set_error(HVK_EINVAL, "hvk_attn_bias_fwd: null pointer or C=%d", C);
-  const int grid = (C + 3) / 4 < 64 ? (C + 3) / 4 : 64;
-  hipLaunchKernelGGL(attn_bias_fwd_kernel, dim3(grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     q_bias, v_bias, proj_bias, proj_w, C, qkv_bias, eff);
+  hipLaunchKernelGGL(attn_bias_fwd_kernel, dim3((C + 3) / 4), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), q_bias, v_bias, proj_bias, proj_w, C, qkv_bias,
+                     eff, dv_zero);
   HVK_CHECK_LAUNCH("hvk_attn_bias_fwd");
   return HVK_OK;
 }
@@ -75,8 +80,6 @@ int hvk_attn_bias_bwd(const float* g, const float* v_bias, const float* proj_w, 
   if (!g || !v_bias || !proj_w || !d_v_bias || !d_proj_w || C <= 0)
     return hvk_set_error(HVK_EINVAL, "hvk_attn_bias_bwd: null pointer or C=%d", C);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(d_v_bias, 0, (size_t)C * sizeof(float), st) != hipSuccess)
-    return hvk_set_error(HVK_EHIP, "hvk_attn_bias_bwd: memset failed");
   hipLaunchKernelGGL(attn_bias_bwd_kernel, dim3((C + kRows - 1) / kRows), dim3(256), 0, st, g, v_bias,
                      proj_w, C, d_proj_bias, d_v_bias, d_proj_w);
   HVK_CHECK_LAUNCH("hvk_attn_bias_bwd");

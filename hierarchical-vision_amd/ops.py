@@ -269,9 +269,11 @@ class AttnBiasFn(torch.autograd.Function):
         qb = _f32(q_bias.detach()) if q_bias is not None else None
         qkv_bias = torch.empty(3 * C, device=v.device, dtype=torch.float32)
         eff = torch.empty(C, device=v.device, dtype=torch.float32)
+        dv = torch.empty(C, device=v.device, dtype=torch.float32)  # zeroed by the launch
         call("hvk_attn_bias_fwd", ptr(qb), ptr(v), ptr(pb), ptr(w), C, ptr(qkv_bias), ptr(eff),
-             stream())
+             ptr(dv), stream())
         ctx.save_for_backward(v, w)
+        ctx.dv = dv
         ctx.has_pb = proj_bias is not None
         ctx.mark_non_differentiable(qkv_bias)
         return qkv_bias, eff
@@ -284,7 +286,7 @@ class AttnBiasFn(torch.autograd.Function):
         g = _f32(g_eff)
         C = v.numel()
         dpb = torch.empty_like(g) if ctx.has_pb else None
-        dv, dw = torch.empty_like(v), torch.empty_like(w)
+        dv, dw = ctx.dv, torch.empty_like(w)
         call("hvk_attn_bias_bwd", ptr(g), ptr(v), ptr(w), C, ptr(dpb), ptr(dv), ptr(dw), stream())
         return dv, dpb, dw, None
 

@@ -146,9 +146,11 @@ int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m
  * Forward: qkv_bias[3C] = (q_bias or 0, 0, 0) and eff[C] = proj_bias (or 0) + proj_w v_bias
  * (proj_w f32 [C, C]): the qkv GEMM's bias and proj's bias with v_bias folded in (softmax
  * rows sum to 1, so P (V + v_bias) = P V + v_bias).  Backward of eff w.r.t. g = d eff:
- * d_proj_bias = g (if not NULL), d_v_bias = proj_w^T g, d_proj_w = g v_bias^T (written). */
+ * d_proj_bias = g (if not NULL), d_v_bias += proj_w^T g (accumulated: pass the dv_zero
+ * buffer the forward zeroed), d_proj_w = g v_bias^T (written). */
 int hvk_attn_bias_fwd(const float* q_bias, const float* v_bias, const float* proj_bias,
-                      const float* proj_w, int C, float* qkv_bias, float* eff, void* stream);
+                      const float* proj_w, int C, float* qkv_bias, float* eff, float* dv_zero,
+                      void* stream);
 int hvk_attn_bias_bwd(const float* g, const float* v_bias, const float* proj_w, int C,
                       float* d_proj_bias, float* d_v_bias, float* d_proj_w, void* stream);
 
