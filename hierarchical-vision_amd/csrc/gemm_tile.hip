@@ -16,6 +16,15 @@
 
 #include "hvk_common.h"
 
+// experiment builds (tools/probe/Makefile, NOT the product): 1 no MFMA, 2 no stores, 3 no DMA,
+// 4 per-workgroup phase timestamps (hvk_gemm_probe_read, tools/gemm_timeline.py)
+#ifndef HVK_GEMM_PROBE
+#define HVK_GEMM_PROBE 0
+#endif
+#if HVK_GEMM_PROBE == 4
+__device__ unsigned long long g_gemm_probe[32768 * 6];
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(3))) void* lds_vptr_t;
@@ -83,6 +92,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     wsrc[i] = (size_t)(n0 + perm_row(row)) * K + 8 * gc;
   }
   auto issue = [&](int kt, int buf) {
+    if (HVK_GEMM_PROBE == 3) return;
     char* base = smem + buf * STAGE_BYTES;
     const int k0 = kt * BK;
 #pragma unroll
@@ -100,6 +110,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = hvk_f32x4{0, 0, 0, 0};
 
+#if HVK_GEMM_PROBE == 4
+  const unsigned long long t0 = wall_clock64();
+  unsigned long long t1 = 0;
+#endif
   issue(0, 0);
   if (KT > 1) issue(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
@@ -110,6 +124,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+#if HVK_GEMM_PROBE == 4
+    if (kt == 0) t1 = wall_clock64();
+#endif
     const uint32_t base = lds_u32(smem) + (kt & 1) * STAGE_BYTES;
     // PIPE: all 16 fragments of the k-step in flight at once, the first half's MFMAs start as
     // soon as their 8 reads are back (lgkmcnt counts in issue order); else read-wait-compute
@@ -134,6 +151,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
       for (int t = 0; t < 4; ++t) {
         af[t] = tie(ra[ks][t]);
         bf[t] = tie(rb[ks][t]);
+      }
+      if (HVK_GEMM_PROBE == 1) {
+        acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].x ^ af[3].y ^ bf[3].y);
+        return;
       }
 #pragma unroll
       for (int a = 0; a < 4; ++a)
@@ -161,6 +182,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     if (kt + 2 < KT) issue(kt + 2, kt & 1);
   }
 
+#if HVK_GEMM_PROBE == 4
+  const unsigned long long t2 = wall_clock64();
+#endif
+  if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
   // EPI 2: the 8 h vectors of this lane, loaded as one batch before the epilogue math
   uint4 hp[EPI == 2 ? 4 : 1][2];
   if (EPI == 2) {
@@ -221,6 +246,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
       }
     }
   }
+#if HVK_GEMM_PROBE == 4
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t3 = wall_clock64();
+  if (threadIdx.x == 0 && blockIdx.x < 32768) {
+    unsigned long long* q = g_gemm_probe + 6 * blockIdx.x;
+    q[0] = t0; q[1] = t1; q[2] = t2; q[3] = t3;
+    q[4] = __builtin_amdgcn_s_getreg(63492);  // HW_ID
+    q[5] = __builtin_amdgcn_s_getreg(63508);  // XCC_ID
+  }
+#endif
 }
 
 static bool tile_pipe() {
@@ -259,6 +294,13 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
 }  // namespace
 
 extern "C" {
+
+#if HVK_GEMM_PROBE == 4
+int hvk_gemm_probe_read(void* dst, int nblocks) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gemm_probe), sizeof(unsigned long long) * 6 * nblocks, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int hvk_gemm_supported(int M, int K, int N) {
   return M > 0 && K >= BK && K % BK == 0 && N % BN == 0 && K <= 8192 && N <= 16384;

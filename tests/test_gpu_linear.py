@@ -107,6 +107,7 @@ def test_mlp_fused_backward_matches_fp32(C, with_b2):
 
 
 @pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (50176, 1536, 384), (12544, 768, 768),
+                                   (12544, 3072, 768), (777, 1536, 2304), (300, 192, 384),
                                    (1000, 64, 128), (300, 128, 256)])
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_gemm_tile_matches_fp32(M, K, N, with_bias):
@@ -126,6 +127,25 @@ def test_gemm_tile_matches_fp32(M, K, N, with_bias):
     torch.cuda.synchronize()
     rel = ((y.float() - ref).norm() / ref.norm()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("N", [384, 256])
+def test_gemm_tile_sparse_pattern_pins_layout(N):
+    """One nonzero token row and one nonzero weight row: the output must be exactly one
+    nonzero element at (token, feature) -- catches permuted rows / columns."""
+    from hvamd import _lib
+    M, K = 3000, 128
+    x = torch.zeros(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(N, K, device="cuda", dtype=torch.bfloat16)
+    t, f = 2777, N - 75
+    x[t] = 1
+    w[f, :64] = 0.5
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), None, _lib.ptr(y), M, K, N, _lib.stream())
+    ref = torch.zeros(M, N, device="cuda")
+    ref[t, f] = 32
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), ref)
 
 
 def test_gemm_tile_gelu_matches_fp32():

@@ -49,7 +49,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--tunable", default=None, help="enable PyTorch TunableOp, results file path")
     ap.add_argument("--only", default=None, help="regex of gemm names to run")
+    ap.add_argument("--lib", default=None, help="load this libhvk build instead (tools/probe)")
     a = ap.parse_args()
+    if a.lib:
+        from hvamd import _lib as L
+        L.LIB_PATH = os.path.abspath(a.lib)
     if a.tunable:
         torch.cuda.tunable.enable(True)
         torch.cuda.tunable.tuning_enable(True)
@@ -61,7 +65,7 @@ def main():
     from hvamd import _lib
     lib = _lib.load()
     tot_h = 0.0
-    print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw | hvk fwd/dx us")
+    print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw | hvk fwd/dx us | tile fwd/dx us")
     import re
     for name, M, K, N, cnt in shapes():
         if a.only and not re.search(a.only, name):
@@ -73,8 +77,17 @@ def main():
         tx = timeit(lambda: torch.mm(dy, w), a.iters)
         tw = timeit(lambda: ops.weight_grad(dy, x), a.iters)
         wt = w.t().contiguous()
-        hf = timeit(lambda: ops.mm_nt(x, w), a.iters) if lib.hvk_linear_supported(M, K, N) else tf
-        hx = timeit(lambda: ops.mm_nt(dy, wt), a.iters) if lib.hvk_linear_supported(M, N, K) else tx
+        hf = timeit(lambda: ops.mm_nt(x, w), a.iters) if ops._native_nt(M, K, N) else tf
+        hx = timeit(lambda: ops.mm_nt(dy, wt), a.iters) if ops._native_nt(M, N, K) else tx
+        def tile(a2, b2):  # hvk_gemm_fwd forced, wherever its tiling divides the shape
+            m, k = a2.shape
+            n = b2.shape[0]
+            if k % 64 or n % 128:
+                return float("nan")
+            y = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+            return timeit(lambda: _lib.call("hvk_gemm_fwd", _lib.ptr(a2), _lib.ptr(b2), None, _lib.ptr(y),
+                                            m, k, n, _lib.stream()), a.iters)
+        tf_t, tx_t = tile(x, w), tile(dy, wt)
         tot_h += (hf + hx + tw) * cnt
         byt = 2 * (M * K + M * N + N * K)
         fl = 2 * M * N * K
@@ -84,7 +97,8 @@ def main():
             tot[k] += t * cnt
             floor[k] += f * cnt / 1e3
         print(f"{name:10s} {M:7d} {K:5d} {N:6d} {cnt:2d} | {tf * 1e3:8.1f} {tx * 1e3:8.1f} {tw * 1e3:8.1f} | "
-              f"{fl_us:6.1f} {fl_us:6.1f} {fw_us:6.1f} | {hf * 1e3:7.1f} {hx * 1e3:7.1f}", flush=True)
+              f"{fl_us:6.1f} {fl_us:6.1f} {fw_us:6.1f} | {hf * 1e3:7.1f} {hx * 1e3:7.1f} | {tf_t * 1e3:7.1f} {tx_t * 1e3:7.1f}",
+              flush=True)
         del x, w, dy
     for k in tot:
         print(f"total {k}: {tot[k]:.3f} ms/step (floor {floor[k]:.3f})")
