@@ -90,6 +90,21 @@ def synthetic_batch(args, tax, rank, device, img=224):
     return x, y
 
 
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "bench_traffic.json")
+TRAFFIC_SOURCE = ("bench_traffic.json: HBM bytes per launch (mean over the step's launches) from "
+                  "rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes over this bench "
+                  "(tools/gpu_traffic.sh); null when that file is absent")
+
+
+def measured_traffic(kernel):
+    """Mean HBM bytes per launch of `kernel` from the committed PMC measurement, or None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            return json.load(f)["kernels"][kernel]["traffic_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def wmsa_algorithmic_bytes(model, batch):
     """Per-step algorithmic HBM bytes of the W-MSA kernels:
     forward 8*T*C (bf16 qkv read 3C + out write C), backward 16*T*C."""
@@ -226,7 +241,7 @@ def main():
         result["roofline"] = {
             "kernel": "wmsa_fwd_ring_kernel<7,3|4> (all %d launches per step)" % n_launch,
             "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic("wmsa_fwd"),
             "algorithmic_bytes_per_step": fwd_bytes,
             "avg_launch_us": round(1000 * fw_ms / fw_n, 2),
             "ms_per_step": round(fw_ms / timed_steps, 3),
@@ -234,10 +249,13 @@ def main():
                        "before the graph capture (replays carry no per-kernel events)" % timed_steps
                        if args.graph else
                        "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps")}
+        if result["roofline"]["traffic"] is not None:
+            result["roofline"]["algorithmic_bytes_per_launch"] = fwd_bytes // n_launch
+            result["roofline"]["traffic_source"] = TRAFFIC_SOURCE
         result["roofline_bwd"] = {
             "kernel": "wmsa_bwd_kernel<7>", "bound": "hbm", "achieved": round(bwd_gbs, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_step": bwd_bytes,
+            "algorithmic_bytes_per_step": bwd_bytes, "traffic": measured_traffic("wmsa_bwd"),
             "avg_launch_us": round(1000 * bw_ms / bw_n, 2),
             "ms_per_step": round(bw_ms / timed_steps, 3)}
     if rank == 0 and world == 1 and args.cpu_baseline:

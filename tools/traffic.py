@@ -1,0 +1,49 @@
+"""HBM traffic per launch of the W-MSA kernels from two rocprofv3 PMC passes over a short
+bench.py run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
+    python tools/traffic.py FETCH_DIR WRITE_DIR [OUT.json]
+Corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the bytes of 16-B-per-lane
+streaming reads (both W-MSA kernels read by 16-B LDS-DMA / global loads) -> x2; WRITE_SIZE is
+exact for 16-B-per-lane stores.  Both counters are in KiB."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_kernel"}
+
+
+def per_kernel(d, counter):
+    out = collections.defaultdict(list)
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            for key, pat in KERNELS.items():
+                if pat in r["Kernel_Name"]:
+                    out[key].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    fetch, write = per_kernel(sys.argv[1], "FETCH_SIZE"), per_kernel(sys.argv[2], "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
+                     "bench.py --steps 2 --warmup 1; FETCH_SIZE x2 (gfx950 16-B/lane reads), KiB -> B",
+           "kernels": {}}
+    for key in KERNELS:
+        f, w = fetch.get(key, []), write.get(key, [])
+        if not f or not w:
+            continue
+        fb = 2 * 1024 * sum(f) / len(f)
+        wb = 1024 * sum(w) / len(w)
+        res["kernels"][key] = {"launches": len(f), "fetch_bytes_per_launch": round(fb),
+                               "write_bytes_per_launch": round(wb),
+                               "traffic_bytes_per_launch": round(fb + wb)}
+    s = json.dumps(res, indent=1)
+    print(s)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
