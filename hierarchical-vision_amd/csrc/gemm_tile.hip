@@ -1,6 +1,6 @@
 // Tiled MFMA GEMM for the compute-heavier SwinV2 Linears on gfx950 (stage 2-3 of SwinV2-T:
-// M = 12544-50176 tokens, K = 384-3072, N = 384-3072), where the weight block no longer fits
-// the skinny kernel's LDS (gemm.hip):
+// M = 12544-50176 tokens, K = 384-3072, N = 384-3072, and the stage-1 N = 192 GEMMs with
+// K = 576-768), where the weight block no longer fits the skinny kernel's LDS (gemm.hip):
 //   Y[M, N] = X[M, K] W[N, K]^T (+ bias[N]) (EPI 0), or the fc1 form h = Y + bias, GELU(h)
 //   (EPI 1) -- F.linear of swinv2.py:58-62, 220, 262 and the input gradients (W = weight^T).
 // 128 x 128 output tile per 256-thread workgroup (2 x 2 waves of 64 x 64), K in steps of 64:
@@ -30,10 +30,15 @@ namespace {
 typedef __attribute__((address_space(3))) void* lds_vptr_t;
 typedef __attribute__((address_space(1))) void* gbl_vptr_t;
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;  // double buffered: 64 KB
+// 2 x 2 waves per 256-thread workgroup; a wave owns 64 rows (4 x-tiles of 16 tokens) and
+// 16 TN columns (TN W-tiles): TN = 4 -> 128 x 128 output tiles (64 KB LDS, double buffered),
+// TN = 6 -> 128 x 192 for N = 192 (80 KB: still two workgroups per CU)
+constexpr int BM = 128, BK = 64;
+constexpr int XTILE_BYTES = BM * BK * 2;  // 16 KB
+template <int TN>
+struct TileCfg {
+  static constexpr int BN = 32 * TN, WTILE = BN * BK * 2, STAGE = WTILE + XTILE_BYTES, LDS = 2 * STAGE;
+};
 
 // LDS row p of a W tile holds W row perm(p) of the tile (see gemm.hip: the accumulator rows
 // 4g + r of tiles 2j, 2j+1 then map to output columns 32j + 8g .. 32j + 8g + 7)
@@ -58,13 +63,15 @@ __device__ __forceinline__ uint4 tie(hvk_u32x4 v) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-template <int EPI, bool PIPE>
+template <int EPI, bool PIPE, int TN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
                                                         const hvk_bf16* __restrict__ Wt,
                                                         const float* __restrict__ bias,
                                                         hvk_bf16* __restrict__ Y,
                                                         hvk_bf16* __restrict__ Y2, int M, int N,
                                                         int K, int mtiles) {
+  using T = TileCfg<TN>;
+  constexpr int BN = T::BN, STAGE_BYTES = T::STAGE, TILE_BYTES = T::WTILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ntiles = N / BN;
   // XCD-aware decode: the n-tiles of one m-tile share blockIdx % 8 (one L2): the X row block
@@ -75,38 +82,43 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const int m0 = mt * BM, n0 = nt * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
-  const int wn = wave & 1, wm = wave >> 1;  // this wave's 64 x 64 sub-tile (n half, m half)
+  const int wn = wave & 1, wm = wave >> 1;  // this wave's 64 x 16TN sub-tile (n half, m half)
   const int KT = K / BK;
 
-  // DMA: tile operand instruction j (0..15) fills LDS rows 8j .. 8j+7; lane L -> row
-  // 8j + L/8, LDS chunk L%8 <- global chunk (L%8) ^ (row & 7).  Wave w issues j = w + 4i.
+  // DMA: operand instruction j fills LDS rows 8j .. 8j+7 of its tile; lane L -> row
+  // 8j + L/8, LDS chunk L%8 <- global chunk (L%8) ^ (row & 7).  Wave w issues j = w + 4i
+  // (4 x-tile and TN W-tile instructions per wave and stage).
   const int lr = lane >> 3, lc = lane & 7;
-  size_t xsrc[4], wsrc[4];
+  size_t xsrc[4], wsrc[TN];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 8 * (wave + 4 * i) + lr;
-    const int gc = lc ^ (row & 7);
     int xr = m0 + row;
     if (xr >= M) xr = M - 1;  // rows past M: any valid row (never stored)
-    xsrc[i] = (size_t)xr * K + 8 * gc;
-    wsrc[i] = (size_t)(n0 + perm_row(row)) * K + 8 * gc;
+    xsrc[i] = (size_t)xr * K + 8 * (lc ^ (row & 7));
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int row = 8 * (wave + 4 * i) + lr;
+    wsrc[i] = (size_t)(n0 + perm_row(row)) * K + 8 * (lc ^ (row & 7));
   }
   auto issue = [&](int kt, int buf) {
     if (HVK_GEMM_PROBE == 3) return;
     char* base = smem + buf * STAGE_BYTES;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = wave + 4 * i;
-      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(Wt + wsrc[i] + k0), (lds_vptr_t)(base + j * 1024), 16, 0, 0);
+    for (int i = 0; i < TN; ++i)
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(Wt + wsrc[i] + k0),
+                                       (lds_vptr_t)(base + (wave + 4 * i) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + xsrc[i] + k0),
-                                       (lds_vptr_t)(base + TILE_BYTES + j * 1024), 16, 0, 0);
-    }
+                                       (lds_vptr_t)(base + TILE_BYTES + (wave + 4 * i) * 1024), 16, 0, 0);
   };
 
-  hvk_f32x4 acc[4][4];
+  hvk_f32x4 acc[TN][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < TN; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = hvk_f32x4{0, 0, 0, 0};
 
@@ -117,9 +129,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   issue(0, 0);
   if (KT > 1) issue(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
-    // this k-step's tile has landed (the next one's 8 DMAs per wave may stay in flight)
+    // this k-step's tile has landed (the next one's TN + 4 DMAs per wave may stay in flight)
     if (kt + 1 < KT)
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TN + 4) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -128,43 +140,46 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     if (kt == 0) t1 = wall_clock64();
 #endif
     const uint32_t base = lds_u32(smem) + (kt & 1) * STAGE_BYTES;
-    // PIPE: all 16 fragments of the k-step in flight at once, the first half's MFMAs start as
-    // soon as their 8 reads are back (lgkmcnt counts in issue order); else read-wait-compute
-    // per half
-    hvk_u32x4 ra[2][4], rb[2][4];
+    // PIPE: all 2 (TN + 4) fragments of the k-step in flight at once, the first half's MFMAs
+    // start as soon as their reads are back (lgkmcnt counts in issue order); else
+    // read-wait-compute per half
+    hvk_u32x4 ra[2][TN], rb[2][4];
     auto read_half = [&](int ks) {
-      // rows 64w + 16t + li (row & 7 = li & 7), chunk 4ks + g swizzled; t in immediates
-      const uint32_t aw = base + (64 * wn + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
+      // rows 16 TN wn + 16t + li (row & 7 = li & 7), chunk 4ks + g swizzled; t in immediates
+      const uint32_t aw = base + (16 * TN * wn + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
       const uint32_t ax = base + TILE_BYTES + (64 * wm + li) * 128 + (((4 * ks + g) ^ (li & 7)) << 4);
       ra[ks][0] = rd128<0>(aw);
       ra[ks][1] = rd128<2048>(aw);
       ra[ks][2] = rd128<4096>(aw);
       ra[ks][3] = rd128<6144>(aw);
+      if constexpr (TN > 4) {
+        ra[ks][4 % TN] = rd128<8192>(aw);
+        ra[ks][5 % TN] = rd128<10240>(aw);
+      }
       rb[ks][0] = rd128<0>(ax);
       rb[ks][1] = rd128<2048>(ax);
       rb[ks][2] = rd128<4096>(ax);
       rb[ks][3] = rd128<6144>(ax);
     };
     auto mfma_half = [&](int ks) {
-      uint4 af[4], bf[4];
+      uint4 af[TN], bf[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        af[t] = tie(ra[ks][t]);
-        bf[t] = tie(rb[ks][t]);
-      }
+      for (int t = 0; t < TN; ++t) af[t] = tie(ra[ks][t]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bf[t] = tie(rb[ks][t]);
       if (HVK_GEMM_PROBE == 1) {
         acc[0][0][0] += __uint_as_float(af[0].x ^ bf[0].x ^ af[3].y ^ bf[3].y);
         return;
       }
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < TN; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = hvk_mfma16(af[a], bf[b], acc[a][b]);
     };
     if (PIPE) {
       read_half(0);
       read_half(1);
-      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TN + 4) : "memory");
       mfma_half(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_half(1);
@@ -187,26 +202,26 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
   // EPI 2: the 8 h vectors of this lane, loaded as one batch before the epilogue math
-  uint4 hp[EPI == 2 ? 4 : 1][2];
+  uint4 hp[EPI == 2 ? 4 : 1][TN / 2];
   if (EPI == 2) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       int row = m0 + 64 * wm + 16 * b + li;
       if (row >= M) row = M - 1;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + n0 + 64 * wn + 32 * j + 8 * g);
+      for (int j = 0; j < TN / 2; ++j)
+        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + n0 + 16 * TN * wn + 32 * j + 8 * g);
     }
   }
   // epilogue: lane (li, g) holds, for m-tile b and n-tile pair (2j, 2j+1), row
-  // m0 + 64wm + 16b + li and columns n0 + 64wn + 32j + 8g .. +7
+  // m0 + 64wm + 16b + li and columns n0 + 16 TN wn + 32j + 8g .. +7
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const int row = m0 + 64 * wm + 16 * b + li;
     if (row >= M) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + 64 * wn + 32 * j + 8 * g;
+    for (int j = 0; j < TN / 2; ++j) {
+      const int col = n0 + 16 * TN * wn + 32 * j + 8 * g;
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -266,29 +281,34 @@ static bool tile_pipe() {
   return v != 0;
 }
 
-template <int EPI, bool PIPE>
+template <int EPI, bool PIPE, int TN>
 int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                int M, int N, int K, hipStream_t st) {
+                 int M, int N, int K, hipStream_t st) {
+  using T = TileCfg<TN>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, PIPE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, PIPE, TN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
     attr = true;
   }
   const int mtiles = (M + BM - 1) / BM;
   const int mpad = (mtiles + 7) / 8 * 8;
-  const dim3 grid(mpad * (N / BN));
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, PIPE>), grid, dim3(256), LDS_BYTES, st, X, W, bias, Y, Y2, M, N, K,
-                     mtiles);
+  const dim3 grid(mpad * (N / T::BN));
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256), T::LDS, st, X, W, bias, Y, Y2, M, N,
+                     K, mtiles);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }
 
+// 128 x 128 tiles where 128 | N, else 128 x 192 (N = 192, 576: the stage-1 input gradients)
 template <int EPI>
 int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                 int M, int N, int K, hipStream_t st) {
-  return tile_pipe() ? launch_tile_<EPI, true>(X, W, bias, Y, Y2, M, N, K, st)
-                     : launch_tile_<EPI, false>(X, W, bias, Y, Y2, M, N, K, st);
+  if (N % TileCfg<4>::BN == 0)
+    return tile_pipe() ? launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st)
+                       : launch_tile_<EPI, false, 4>(X, W, bias, Y, Y2, M, N, K, st);
+  return tile_pipe() ? launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st)
+                     : launch_tile_<EPI, false, 6>(X, W, bias, Y, Y2, M, N, K, st);
 }
 
 }  // namespace
@@ -303,7 +323,8 @@ int hvk_gemm_probe_read(void* dst, int nblocks) {
 #endif
 
 int hvk_gemm_supported(int M, int K, int N) {
-  return M > 0 && K >= BK && K % BK == 0 && N % BN == 0 && K <= 8192 && N <= 16384;
+  return M > 0 && K >= BK && K % BK == 0 && (N % TileCfg<4>::BN == 0 || N % TileCfg<6>::BN == 0) &&
+         K <= 8192 && N <= 16384;
 }
 
 int hvk_gemm_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,

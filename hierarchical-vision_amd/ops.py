@@ -163,13 +163,21 @@ def _linear_native(M, K, N):
     return ok and M > 0
 
 
+_TILE_ROUTE = int(os.environ.get("HVK_TILE_ROUTE", "1"))
+
+
 def _tile_ok(M, K, N):
     """libhvk's tiled MFMA GEMM (hvk_gemm_fwd) where it measured faster than the library GEMM
-    (tools/bench_skinny.py): the stage-2 shapes with K <= 1152 and the 768 x 768 stage-3
-    projection; the wider stage-3 shapes stay on the library."""
-    if K % 64 or N % 128 or M <= 0:
+    (tools/bench_gemm.py): the stage-2 shapes (K <= 1536, fc2 forward and fc1 input gradient
+    included), the stage-1 N = 192 shapes with K = 576 / 768 (128 x 192 tiles) and the
+    768 x 768 stage-3 projection; the wider stage-3 shapes stay on the library."""
+    if K % 64 or M <= 0:
         return False
-    return (M >= 32768 and K <= 1152) or (K == 768 and N == 768)
+    if _TILE_ROUTE == 0:  # the earlier routing (A/B experiments): stage 2 with K <= 1152
+        return not N % 128 and ((M >= 32768 and K <= 1152) or (K == 768 and N == 768))
+    if N % 128:  # the 128 x 192 tile: stage-1 fc2 forward and qkv / fc1 input gradients
+        return N == 192 and K in (576, 768) and M >= 32768
+    return (M >= 32768 and K <= 1536) or (K == 768 and N == 768)
 
 
 def _native_nt(M, K, N):
@@ -276,6 +284,7 @@ class AttnBiasFn(torch.autograd.Function):
         ctx.dv = dv
         ctx.has_pb = proj_bias is not None
         ctx.mark_non_differentiable(qkv_bias)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the qkv bias output
         return qkv_bias, eff
 
     @staticmethod
@@ -287,6 +296,7 @@ class AttnBiasFn(torch.autograd.Function):
         C = v.numel()
         dpb = torch.empty_like(g) if ctx.has_pb else None
         dv, dw = ctx.dv, torch.empty_like(w)
+        ctx.dv = None  # the only reference left is the returned one: AccumulateGrad steals it
         call("hvk_attn_bias_bwd", ptr(g), ptr(v), ptr(w), C, ptr(dpb), ptr(dv), ptr(dw), stream())
         return dv, dpb, dw, None
 
@@ -620,6 +630,18 @@ class PatchMergeGather(torch.autograd.Function):
         gx = torch.empty((B, H * W, C), device=g.device, dtype=torch.bfloat16)
         call("hvk_patch_merge_scatter", ptr(g), ptr(gx), B, H, W, C, stream())
         return gx, None, None
+
+
+def patchify_bf16(x, patch):
+    """f32 images [B, C, H, W] -> bf16 token-major patches [B, (H/p)(W/p), C p p] in the
+    Conv2d weight's (c, py, px) order: x.to(bfloat16) + permute + reshape in one kernel
+    (swinv2.py:652-660).  Images carry no gradient; with one, or another patch size / channel
+    count, the caller keeps the torch form."""
+    B, C, H, W = x.shape
+    out = torch.empty((B, (H // patch) * (W // patch), C * patch * patch), device=x.device,
+                      dtype=torch.bfloat16)
+    call("hvk_patchify_bf16", ptr(x.contiguous()), ptr(out), B, C, H, W, stream())
+    return out
 
 
 def patch_merge_gather(x, H, W):

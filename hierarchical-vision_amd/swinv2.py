@@ -435,8 +435,12 @@ class PatchEmbed(nn.Module):
             f"Input image size ({H}*{W}) doesn't match model ({self.img_size[0]}*{self.img_size[1]})."
         ph, pw = self.patch_size
         gh, gw = self.patches_resolution
-        xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
-        patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * ph * pw)
+        if (x.is_cuda and torch.is_autocast_enabled() and x.dtype == torch.float32 and C == 3
+                and ph == pw == 4 and not x.requires_grad):
+            patches = ops.patchify_bf16(x, 4)  # cast + patch gather in one launch
+        else:
+            xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
+            patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * ph * pw)
         w = self.proj.weight.reshape(self.embed_dim, -1)
         if self.norm is None:
             return _as_stream(ops.linear(patches, w, self.proj.bias))

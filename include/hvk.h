@@ -211,6 +211,10 @@ int hvk_bias_gelu_bwd(const void* h, const float* bias, const void* gy, void* gh
  * (dh, dw)_k = (0,0), (1,0), (0,1), (1,1); x: bf16 [B, H*W, C], out: bf16 [B, H*W/4, 4C].
  * scatter is the exact inverse (a permutation: every element written once). */
 int hvk_patch_merge_gather(const void* x, void* out, int B, int H, int W, int C, void* stream);
+/* PatchEmbed input (swinv2.py:652-660, the 4x4/s4 Conv2d as a GEMM): f32 images
+ * x [B, C, H, W] -> bf16 patches [B, (H/4)(W/4), C*16] in (c, py, px) order, rounded to
+ * nearest even (x.to(bfloat16) + permute + reshape in one pass).  C = 3 is built. */
+int hvk_patchify_bf16(const float* x, void* out, int B, int C, int H, int W, void* stream);
 int hvk_patch_merge_scatter(const void* gout, void* gx, int B, int H, int W, int C,
                             void* stream);
 

@@ -108,11 +108,13 @@ def test_mlp_fused_backward_matches_fp32(C, with_b2):
 
 @pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (50176, 1536, 384), (12544, 768, 768),
                                    (12544, 3072, 768), (777, 1536, 2304), (300, 192, 384),
-                                   (1000, 64, 128), (300, 128, 256)])
+                                   (1000, 64, 128), (300, 128, 256), (20000, 768, 192),
+                                   (1000, 576, 192), (777, 64, 192)])
 @pytest.mark.parametrize("with_bias", [False, True])
 def test_gemm_tile_matches_fp32(M, K, N, with_bias):
-    """Tiled MFMA GEMM (hvk_gemm_fwd) vs fp32 matmul of the same bf16 operands, including
-    row counts that are not a multiple of the 128-row tile."""
+    """Tiled MFMA GEMM (hvk_gemm_fwd) vs fp32 matmul of the same bf16 operands, on both tile
+    widths (128 columns where 128 | N, else 192), including row counts that are not a
+    multiple of the 128-row tile."""
     from hvamd import _lib
     lib = _lib.load()
     assert lib.hvk_gemm_supported(M, K, N)
@@ -129,7 +131,7 @@ def test_gemm_tile_matches_fp32(M, K, N, with_bias):
     assert rel < 1e-2, rel
 
 
-@pytest.mark.parametrize("N", [384, 256])
+@pytest.mark.parametrize("N", [384, 256, 192])
 def test_gemm_tile_sparse_pattern_pins_layout(N):
     """One nonzero token row and one nonzero weight row: the output must be exactly one
     nonzero element at (token, feature) -- catches permuted rows / columns."""

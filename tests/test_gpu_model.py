@@ -96,6 +96,16 @@ def test_patch_merge_gather_bit_exact():
     assert torch.equal(xg.grad, x)  # scatter is the exact inverse permutation
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 224, 224), (3, 32, 48), (1, 4, 4)])
+def test_patchify_bf16_bit_exact(B, H, W):
+    """hvk_patchify_bf16 == x.to(bfloat16) + the (c, py, px) patch permute of PatchEmbed."""
+    import hvamd.ops as ops
+    x = torch.randn(B, 3, H, W, device="cuda") * 3
+    out = ops.patchify_bf16(x, 4)
+    ref = x.bfloat16().reshape(B, 3, H // 4, 4, W // 4, 4).permute(0, 2, 4, 1, 3, 5).reshape(B, -1, 48)
+    assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("C", [96, 192, 384, 768, 1024, 64])
 def test_layernorm_residual_vs_torch(C):
     import hvamd.ops as ops
