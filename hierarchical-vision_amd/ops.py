@@ -164,6 +164,7 @@ def _linear_native(M, K, N):
 
 
 _TILE_ROUTE = int(os.environ.get("HVK_TILE_ROUTE", "1"))
+_TILE_S3 = int(os.environ.get("HVK_TILE_S3", "1"))
 
 
 def _tile_ok(M, K, N):
@@ -177,6 +178,8 @@ def _tile_ok(M, K, N):
         return not N % 128 and ((M >= 32768 and K <= 1152) or (K == 768 and N == 768))
     if N % 128:  # the 128 x 192 tile: stage-1 fc2 forward and qkv / fc1 input gradients
         return N == 192 and K in (576, 768) and M >= 32768
+    if K == 768 and N == 3072 and _TILE_S3:  # stage-3 fc1 + GELU and fc2 input grad x GELU'
+        return True
     return (M >= 32768 and K <= 1536) or (K == 768 and N == 768)
 
 
@@ -598,14 +601,14 @@ class MlpFn(torch.autograd.Function):
 
 
 def mlp(x, w1, b1, w2, b2=None):
-    """fc2(GELU(fc1(x))): the fused forward/backward kernels where built (stage 0-1 shapes),
-    else linear_gelu + linear."""
+    """fc2(GELU(fc1(x))): the fused forward/backward kernels where built (skinny for stage 0-1,
+    tiled for stage 2-3), else linear_gelu + linear."""
     N1, K = w1.shape
     M = x.numel() // K
     lib = _lib.load()
     if (b1 is not None and ((K in (96, 192) and lib.hvk_linear_gelu_supported(M, K, N1))
                             or _tile_ok(M, K, N1))
-            and lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1)):
+            and (lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1) or _tile_ok(M, w2.shape[0], N1))):
         return MlpFn.apply(x, w1, b1, w2, b2)
     return linear(linear_gelu(x, w1, b1), w2, b2)
 
