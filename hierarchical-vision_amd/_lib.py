@@ -57,6 +57,9 @@ SIGNATURES = {
     "hvk_bias_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _p, _sz, _i, _i, _p]),
     "hvk_patch_merge_gather": (_i, [_p, _p, _i, _i, _i, _i, _p]),
     "hvk_patch_merge_scatter": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "hvk_ln_pool_supported": (_i, [_i]),
+    "hvk_ln_pool_fwd": (_i, [_p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p, _p, _p]),
+    "hvk_ln_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
     "hvk_patchify_bf16": (_i, [_p, _p, _i, _i, _i, _i, _p]),
     "hvk_multitask_ce_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "hvk_multitask_ce_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),

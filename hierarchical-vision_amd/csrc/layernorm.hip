@@ -269,6 +269,141 @@ int check_shape(const char* who, int rows, int C, int rps, int& ept, int& tpr) {
   return HVK_OK;
 }
 
+// Final LayerNorm + token average pool (swinv2.py:833-835): y[b] = mean_t LN(x[b, t, :]) for
+// the f32 stream x [B, T, C].  One 256-thread workgroup per sample; a wave normalizes rows
+// t = wave, wave + 4, ... with its lanes holding V float4 columns each (C = 256 V); the
+// per-sample sums of x-hat are kept (xsum) -- they are all the backward needs besides the
+// row statistics: y = gamma * xsum / T + beta, d gamma = sum_b (dy_b / T) xsum_b, d beta =
+// sum_b dy_b.  Workgroup 0 also zeroes the backward's d gamma / d beta accumulators.
+template <int V>
+__global__ __launch_bounds__(256) void ln_pool_fwd_kernel(const float4* __restrict__ x, const float4* __restrict__ gamma,
+                                                          const float4* __restrict__ beta, int T, float eps,
+                                                          float4* __restrict__ y, float4* __restrict__ xsum,
+                                                          float* __restrict__ mean, float* __restrict__ rstd,
+                                                          float4* __restrict__ zero_g, float4* __restrict__ zero_b) {
+  constexpr int C4 = 64 * V;
+  __shared__ float4 red[4][C4];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (b == 0)
+    for (int i = threadIdx.x; i < C4; i += 256) zero_g[i] = zero_b[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float invC = 1.f / (4 * C4);
+  float4 acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t = wave; t < T; t += 4) {
+    const float4* xr = x + ((size_t)b * T + t) * C4;
+    float4 v[V];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      v[j] = xr[lane + 64 * j];
+      s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    const float mu = s * invC;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      v[j].x -= mu; v[j].y -= mu; v[j].z -= mu; v[j].w -= mu;
+      q += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+    const float rs = rsqrtf(q * invC + eps);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      acc[j].x += v[j].x * rs; acc[j].y += v[j].y * rs; acc[j].z += v[j].z * rs; acc[j].w += v[j].w * rs;
+    }
+    if (lane == 0) {
+      mean[(size_t)b * T + t] = mu;
+      rstd[(size_t)b * T + t] = rs;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[wave][lane + 64 * j] = acc[j];
+  __syncthreads();
+  const float invT = 1.f / T;
+  for (int i = threadIdx.x; i < C4; i += 256) {
+    float4 a = red[0][i];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 r = red[w][i];
+      a.x += r.x; a.y += r.y; a.z += r.z; a.w += r.w;
+    }
+    xsum[(size_t)b * C4 + i] = a;
+    const float4 g = gamma[i], be = beta[i];
+    y[(size_t)b * C4 + i] = make_float4(g.x * a.x * invT + be.x, g.y * a.y * invT + be.y,
+                                        g.z * a.z * invT + be.z, g.w * a.w * invT + be.w);
+  }
+}
+
+// backward: every row of sample b receives g = dy_b / T; dx = rstd (g gamma - mean_c(g gamma)
+// - xhat mean_c(g gamma xhat)); d gamma, d beta by one float atomic per column and sample
+template <int V>
+__global__ __launch_bounds__(256) void ln_pool_bwd_kernel(const float4* __restrict__ x, const float4* __restrict__ gamma,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          const float4* __restrict__ xsum, const float4* __restrict__ dy,
+                                                          int T, float4* __restrict__ dx, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta) {
+  constexpr int C4 = 64 * V;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float invT = 1.f / T, invC = 1.f / (4 * C4);
+  float4 gg[V];
+  float s1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const float4 d = dy[(size_t)b * C4 + lane + 64 * j], g = gamma[lane + 64 * j];
+    gg[j] = make_float4(d.x * invT * g.x, d.y * invT * g.y, d.z * invT * g.z, d.w * invT * g.w);
+    s1 += (gg[j].x + gg[j].y) + (gg[j].z + gg[j].w);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s1 += __shfl_xor(s1, m);
+  s1 *= invC;
+  for (int t = wave; t < T; t += 4) {
+    const size_t r = (size_t)b * T + t;
+    const float mu = mean[r], rs = rstd[r];
+    const float4* xr = x + r * C4;
+    float4 h[V];
+    float s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float4 v = xr[lane + 64 * j];
+      h[j] = make_float4((v.x - mu) * rs, (v.y - mu) * rs, (v.z - mu) * rs, (v.w - mu) * rs);
+      s2 += (gg[j].x * h[j].x + gg[j].y * h[j].y) + (gg[j].z * h[j].z + gg[j].w * h[j].w);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s2 += __shfl_xor(s2, m);
+    s2 *= invC;
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+      dx[r * C4 + lane + 64 * j] =
+          make_float4(rs * (gg[j].x - s1 - h[j].x * s2), rs * (gg[j].y - s1 - h[j].y * s2),
+                      rs * (gg[j].z - s1 - h[j].z * s2), rs * (gg[j].w - s1 - h[j].w * s2));
+  }
+  for (int i = threadIdx.x; i < C4; i += 256) {
+    const float4 d = dy[(size_t)b * C4 + i], xs = xsum[(size_t)b * C4 + i];
+    atomicAdd(dgamma + 4 * i, d.x * invT * xs.x);
+    atomicAdd(dgamma + 4 * i + 1, d.y * invT * xs.y);
+    atomicAdd(dgamma + 4 * i + 2, d.z * invT * xs.z);
+    atomicAdd(dgamma + 4 * i + 3, d.w * invT * xs.w);
+    atomicAdd(dbeta + 4 * i, d.x);
+    atomicAdd(dbeta + 4 * i + 1, d.y);
+    atomicAdd(dbeta + 4 * i + 2, d.z);
+    atomicAdd(dbeta + 4 * i + 3, d.w);
+  }
+}
+
+#define HVK_POOL_DISPATCH(KERNEL, ...)                                                          \
+  switch (C / 256) {                                                                           \
+    case 1: hipLaunchKernelGGL((KERNEL<1>), dim3(B), dim3(256), 0, st, __VA_ARGS__); break;   \
+    case 2: hipLaunchKernelGGL((KERNEL<2>), dim3(B), dim3(256), 0, st, __VA_ARGS__); break;   \
+    case 3: hipLaunchKernelGGL((KERNEL<3>), dim3(B), dim3(256), 0, st, __VA_ARGS__); break;   \
+    case 4: hipLaunchKernelGGL((KERNEL<4>), dim3(B), dim3(256), 0, st, __VA_ARGS__); break;   \
+    case 6: hipLaunchKernelGGL((KERNEL<6>), dim3(B), dim3(256), 0, st, __VA_ARGS__); break;   \
+    default: return hvk_set_error(HVK_EUNSUPPORTED, "ln_pool: C=%d", C);                      \
+  }
+
 }  // namespace
 
 extern "C" {
@@ -319,6 +454,38 @@ int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
   hipLaunchKernelGGL(colsum_kernel, dim3((3 * C + 63) / 64, kRedRowGroups), dim3(64), 0, st,
                      workspace, grid, 3 * C, dgamma, dbeta, dabias, C);
   HVK_CHECK_LAUNCH("ln_bwd_colsum");
+  return HVK_OK;
+}
+
+int hvk_ln_pool_supported(int C) { return C > 0 && C % 256 == 0 && (C / 256 <= 4 || C / 256 == 6); }
+
+int hvk_ln_pool_fwd(const float* x, const float* gamma, const float* beta, int B, int T, int C, float eps,
+                    float* y, float* xsum, float* mean, float* rstd, float* dgamma_zero, float* dbeta_zero,
+                    void* stream) {
+  if (!x || !gamma || !beta || !y || !xsum || !mean || !rstd || !dgamma_zero || !dbeta_zero)
+    return hvk_set_error(HVK_EINVAL, "hvk_ln_pool_fwd: null pointer");
+  if (B <= 0 || T <= 0 || !hvk_ln_pool_supported(C))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_ln_pool_fwd: B=%d T=%d C=%d", B, T, C);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HVK_POOL_DISPATCH(ln_pool_fwd_kernel, reinterpret_cast<const float4*>(x), reinterpret_cast<const float4*>(gamma),
+                    reinterpret_cast<const float4*>(beta), T, eps, reinterpret_cast<float4*>(y),
+                    reinterpret_cast<float4*>(xsum), mean, rstd, reinterpret_cast<float4*>(dgamma_zero),
+                    reinterpret_cast<float4*>(dbeta_zero));
+  HVK_CHECK_LAUNCH("ln_pool_fwd");
+  return HVK_OK;
+}
+
+int hvk_ln_pool_bwd(const float* x, const float* gamma, const float* mean, const float* rstd, const float* xsum,
+                    const float* dy, int B, int T, int C, float* dx, float* dgamma, float* dbeta, void* stream) {
+  if (!x || !gamma || !mean || !rstd || !xsum || !dy || !dx || !dgamma || !dbeta)
+    return hvk_set_error(HVK_EINVAL, "hvk_ln_pool_bwd: null pointer");
+  if (B <= 0 || T <= 0 || !hvk_ln_pool_supported(C))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_ln_pool_bwd: B=%d T=%d C=%d", B, T, C);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HVK_POOL_DISPATCH(ln_pool_bwd_kernel, reinterpret_cast<const float4*>(x), reinterpret_cast<const float4*>(gamma),
+                    mean, rstd, reinterpret_cast<const float4*>(xsum), reinterpret_cast<const float4*>(dy), T,
+                    reinterpret_cast<float4*>(dx), dgamma, dbeta);
+  HVK_CHECK_LAUNCH("ln_pool_bwd");
   return HVK_OK;
 }
 

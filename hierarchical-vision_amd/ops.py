@@ -477,6 +477,43 @@ def layer_norm_residual(a, x0, gamma, beta, sample_scale=None, rows_per_sample=1
 
 
 # --------------------------------------------------------------------------- MLP activation
+class NormPool(torch.autograd.Function):
+    """mean over tokens of LayerNorm(x) for the f32 stream x [B, T, C] (the final norm and
+    the average pool, swinv2.py:833-835) as one kernel each way (hvk_ln_pool_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps):
+        x = _f32(x)
+        B, T, C = x.shape
+        dev = x.device
+        y = torch.empty((B, C), device=dev, dtype=torch.float32)
+        xsum = torch.empty_like(y)
+        mean = torch.empty(B * T, device=dev, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        dg = torch.empty(C, device=dev, dtype=torch.float32)  # zeroed by the launch
+        db = torch.empty_like(dg)
+        call("hvk_ln_pool_fwd", ptr(x), ptr(_f32(gamma)), ptr(_f32(beta)), B, T, C, float(eps), ptr(y),
+             ptr(xsum), ptr(mean), ptr(rstd), ptr(dg), ptr(db), stream())
+        ctx.save_for_backward(x, gamma, mean, rstd, xsum)
+        ctx.acc = (dg, db)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, rstd, xsum = ctx.saved_tensors
+        dg, db = ctx.acc
+        ctx.acc = None  # returned below as the only references: AccumulateGrad steals them
+        B, T, C = x.shape
+        dx = torch.empty_like(x)
+        call("hvk_ln_pool_bwd", ptr(x), ptr(_f32(gamma)), ptr(mean), ptr(rstd), ptr(xsum),
+             ptr(_f32(dy)), B, T, C, ptr(dx), ptr(dg), ptr(db), stream())
+        return dx, dg, db, None
+
+
+def norm_pool(x, gamma, beta, eps):
+    return NormPool.apply(x, gamma, beta, eps)
+
+
 class BiasGelu(torch.autograd.Function):
     """y = GELU(h + b) (exact erf form); backward also returns db (column sums)."""
 

@@ -19,6 +19,7 @@ block is re-planned around the hardware:
   are plain library GEMMs (hipBLASLt via torch) in bf16 under autocast.
 """
 import dataclasses
+import os
 import re
 from typing import NamedTuple
 
@@ -458,6 +459,13 @@ class PatchEmbed(nn.Module):
         return f + (Ho * Wo * self.embed_dim if self.norm is not None else 0)
 
 
+def _lib_ln_pool_ok(C):
+    """The fused final-norm + pool kernel is built for C (HVK_NORM_POOL=0: the torch form, for
+    A/B runs)."""
+    from . import _lib
+    return os.environ.get("HVK_NORM_POOL", "1") != "0" and bool(_lib.load().hvk_ln_pool_supported(C))
+
+
 class SwinTransformerV2(nn.Module):
     """SwinV2 backbone + flat or multitask head (swinv2.py:673-867)."""
 
@@ -572,10 +580,14 @@ class SwinTransformerV2(nn.Module):
             s = layer.forward_stream(s)
             if output_activations:
                 acts.append(s.f32)
-        with torch.autocast(device_type=x.device.type, enabled=False):
-            y = F.layer_norm(s.f32, (self.num_features,), self.norm.weight, self.norm.bias,
-                             self.norm.eps)
-        y = y.mean(dim=1)  # avgpool over tokens (swinv2.py:834-835)
+        if (s.f32.is_cuda and isinstance(self.norm, nn.LayerNorm) and self.norm.elementwise_affine
+                and _lib_ln_pool_ok(self.num_features)):
+            y = ops.norm_pool(s.f32, self.norm.weight, self.norm.bias, self.norm.eps)  # one kernel
+        else:
+            with torch.autocast(device_type=x.device.type, enabled=False):
+                y = F.layer_norm(s.f32, (self.num_features,), self.norm.weight, self.norm.bias,
+                                 self.norm.eps)
+            y = y.mean(dim=1)  # avgpool over tokens (swinv2.py:834-835)
         return (y, acts) if output_activations else y
 
     def forward_head(self, x, pre_logits=False):

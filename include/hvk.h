@@ -197,6 +197,18 @@ int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
                         float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
                         float* workspace, size_t workspace_bytes, void* stream);
 
+/* Final LayerNorm + token average pool (swinv2.py:833-835): y [B, C] = mean over T of
+ * LN(x [B, T, C] f32) (eps, gamma, beta).  The forward keeps xsum [B, C] = sum_t xhat and
+ * the row statistics mean / rstd [B*T] for the backward, and zeroes dgamma_zero / dbeta_zero
+ * [C], the accumulators hvk_ln_pool_bwd adds d gamma / d beta into (float atomics).
+ * hvk_ln_pool_supported(C): C a multiple of 256, C / 256 in 1..4 or 6. */
+int hvk_ln_pool_supported(int C);
+int hvk_ln_pool_fwd(const float* x, const float* gamma, const float* beta, int B, int T, int C, float eps,
+                    float* y, float* xsum, float* mean, float* rstd, float* dgamma_zero, float* dbeta_zero,
+                    void* stream);
+int hvk_ln_pool_bwd(const float* x, const float* gamma, const float* mean, const float* rstd, const float* xsum,
+                    const float* dy, int B, int T, int C, float* dx, float* dgamma, float* dbeta, void* stream);
+
 /* ---- MLP activation: y = GELU(h + bias), exact erf form (swinv2.py:60-62, nn.GELU) ---
  * h: bf16 [rows, N] = fc1 GEMM output without bias; bias: f32 [N] or NULL; y: bf16.
  * Backward: gh = gy * GELU'(h + bias) (bf16) and dbias = column sums of gh (f32 [N],

@@ -96,6 +96,27 @@ def test_patch_merge_gather_bit_exact():
     assert torch.equal(xg.grad, x)  # scatter is the exact inverse permutation
 
 
+@pytest.mark.parametrize("B,T,C", [(256, 49, 768), (3, 5, 256), (2, 64, 1024), (4, 7, 1536)])
+def test_norm_pool_vs_torch(B, T, C):
+    """Final LayerNorm + token mean (hvk_ln_pool_fwd / _bwd) vs torch f32 autograd of
+    F.layer_norm(...).mean(1): output, dx, d gamma, d beta (swinv2.py:833-835)."""
+    import hvamd.ops as ops
+    g = torch.Generator(device="cuda").manual_seed(B + T + C)
+    x = (torch.randn(B, T, C, device="cuda", generator=g) * 2 + 0.5).requires_grad_(True)
+    gm = (1 + 0.1 * torch.randn(C, device="cuda", generator=g)).requires_grad_(True)
+    bt = (0.1 * torch.randn(C, device="cuda", generator=g)).requires_grad_(True)
+    dy = torch.randn(B, C, device="cuda", generator=g)
+    y = ops.norm_pool(x, gm, bt, 1e-5)
+    y.backward(dy)
+    xr, gr, br = (t.detach().clone().requires_grad_(True) for t in (x, gm, bt))
+    yr = torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-5).mean(1)
+    yr.backward(dy)
+    for name, mine, ref in [("y", y, yr), ("dx", x.grad, xr.grad), ("dgamma", gm.grad, gr.grad),
+                            ("dbeta", bt.grad, br.grad)]:
+        rel = ((mine - ref).norm() / ref.norm()).item()
+        assert rel < 1e-5, (name, rel)
+
+
 @pytest.mark.parametrize("B,H,W", [(2, 224, 224), (3, 32, 48), (1, 4, 4)])
 def test_patchify_bf16_bit_exact(B, H, W):
     """hvk_patchify_bf16 == x.to(bfloat16) + the (c, py, px) patch permute of PatchEmbed."""
