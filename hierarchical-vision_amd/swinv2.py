@@ -556,7 +556,8 @@ class SwinTransformerV2(nn.Module):
 
     def _gemm_weights(self):
         """The f32 master weights every GEMM of a forward casts to bf16 (patch embed, qkv,
-        proj, fc1, fc2, reductions), refreshed together by ops.prepare_weights."""
+        proj, fc1, fc2, reductions, a single Linear head), refreshed together by
+        ops.prepare_weights."""
         ws = [self.patch_embed.proj.weight.reshape(self.patch_embed.embed_dim, -1)]
         for m in self.modules():
             if isinstance(m, WindowAttention):
@@ -565,6 +566,8 @@ class SwinTransformerV2(nn.Module):
                 ws += [m.fc1.weight, m.fc2.weight]
             elif isinstance(m, PatchMerging):
                 ws.append(m.reduction.weight)
+        if isinstance(self.head, nn.Linear):
+            ws.append(self.head.weight)
         return [w for w in ws if w.dtype == torch.float32 and w.is_contiguous()]
 
     def forward_features(self, x, output_activations=False):
@@ -590,11 +593,18 @@ class SwinTransformerV2(nn.Module):
             y = y.mean(dim=1)  # avgpool over tokens (swinv2.py:834-835)
         return (y, acts) if output_activations else y
 
+    def _head(self, x):
+        """The classifier: a single Linear runs as ops.linear under autocast (the step's
+        prepared bf16 weight, f32 dW straight from the GEMM, no per-call casts)."""
+        if isinstance(self.head, nn.Linear) and x.is_cuda and torch.is_autocast_enabled():
+            return ops.linear(x, self.head.weight, self.head.bias)
+        return self.head(x)
+
     def forward_head(self, x, pre_logits=False):
-        return x if pre_logits else self.head(x)
+        return x if pre_logits else self._head(x)
 
     def forward(self, x):
-        return self.head(self.forward_features(x))
+        return self._head(self.forward_features(x))
 
     def flops(self):
         f = self.patch_embed.flops() + sum(layer.flops() for layer in self.layers)
