@@ -300,11 +300,19 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   return HVK_OK;
 }
 
-// 128 x 128 tiles where 128 | N, else 128 x 192 (N = 192, 576: the stage-1 input gradients)
+// 128 x 128 or 128 x 192 tiles
 template <int EPI>
 int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                 int M, int N, int K, hipStream_t st) {
-  if (N % TileCfg<4>::BN == 0)
+  // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1536 case
+  // (tools/bench_gemm.py, interleaved: 3-25 % faster on the stage-2/3 shapes, 6 % slower on
+  // the stage-2 projection); HVK_TILE_WIDE=0 / 1 forces 128 / 192 columns where both divide N
+  static const int force = [] {
+    const char* e = getenv("HVK_TILE_WIDE");
+    return e ? atoi(e) : -1;
+  }();
+  const bool wide = N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536));
+  if (N % TileCfg<4>::BN == 0 && !wide)
     return tile_pipe() ? launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st)
                        : launch_tile_<EPI, false, 4>(X, W, bias, Y, Y2, M, N, K, st);
   return tile_pipe() ? launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st)

@@ -170,15 +170,15 @@ _TILE_S3 = int(os.environ.get("HVK_TILE_S3", "1"))
 def _tile_ok(M, K, N):
     """libhvk's tiled MFMA GEMM (hvk_gemm_fwd) where it measured faster than the library GEMM
     (tools/bench_gemm.py): the stage-2 shapes (K <= 1536, fc2 forward and fc1 input gradient
-    included), the stage-1 N = 192 shapes with K = 576 / 768 (128 x 192 tiles) and the
-    768 x 768 stage-3 projection; the wider stage-3 shapes stay on the library."""
+    included), the stage-1 N = 192 shapes with K = 576 / 768, and every stage-3 shape (and
+    the stage-2 PatchMerging) with 192 | N, on 128 x 192 tiles."""
     if K % 64 or M <= 0:
         return False
     if _TILE_ROUTE == 0:  # the earlier routing (A/B experiments): stage 2 with K <= 1152
         return not N % 128 and ((M >= 32768 and K <= 1152) or (K == 768 and N == 768))
     if N % 128:  # the 128 x 192 tile: stage-1 fc2 forward and qkv / fc1 input gradients
         return N == 192 and K in (576, 768) and M >= 32768
-    if K == 768 and N == 3072 and _TILE_S3:  # stage-3 fc1 + GELU and fc2 input grad x GELU'
+    if _TILE_S3 and M >= 8192 and N % 192 == 0:  # stage 3 and its PatchMerging (128 x 192 tiles)
         return True
     return (M >= 32768 and K <= 1536) or (K == 768 and N == 768)
 
