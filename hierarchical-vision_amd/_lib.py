@@ -39,6 +39,10 @@ SIGNATURES = {
     "hvk_gemm_gelu_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_weight_grad_supported": (_i, [_i, _i, _i]),
     "hvk_cast_weights": (_i, [_i, _p, _p, _p, _p, _p, _p]),
+    "hvk_block_bias_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p,
+                                _p]),
+    "hvk_block_bias_bwd": (_i, [_p, _p, _p, _i, _p, _p, _p, _p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p,
+                                _p, _p, _p, _p, _p, _sz, _p]),
     "hvk_attn_bias_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "hvk_attn_bias_bwd": (_i, [_p, _p, _p, _i, _p, _p, _p, _p]),
     "hvk_sgdw_workspace_bytes": (_sz, [_i, _p]),

@@ -5,58 +5,22 @@
 //   eff = proj.bias + W_proj v_bias      (f32, [C])
 // backward: d proj.bias = g, d v_bias = W_proj^T g, d W_proj = g v_bias^T (this term only;
 // autograd adds the proj GEMM's own weight gradient).
-#include "hvk_common.h"
+#include "block_bias.h"
 
 namespace {
 
-__global__ __launch_bounds__(256) void attn_bias_fwd_kernel(const float* __restrict__ qb,
-                                                            const float* __restrict__ vb,
-                                                            const float* __restrict__ pb,
-                                                            const float* __restrict__ w, int C,
-                                                            float* __restrict__ qkv_bias,
-                                                            float* __restrict__ eff,
+__global__ __launch_bounds__(256) void attn_bias_fwd_kernel(const float* __restrict__ qb, const float* __restrict__ vb,
+                                                            const float* __restrict__ pb, const float* __restrict__ w,
+                                                            int C, float* __restrict__ qkv_bias, float* __restrict__ eff,
                                                             float* __restrict__ dv_zero) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < 3 * C; i += gridDim.x * 256) {
-    qkv_bias[i] = (i < C && qb) ? qb[i] : 0.f;
-    if (dv_zero && i < C) dv_zero[i] = 0.f;  // the backward's d v_bias accumulator
-  }
-  // one wave per output row n: lanes stride over k, wave reduction
-  const int lane = threadIdx.x & 63;
-  for (int n = blockIdx.x * 4 + (threadIdx.x >> 6); n < C; n += gridDim.x * 4) {
-    float s = 0.f;
-    for (int k = lane; k < C; k += 64) s = fmaf(w[(size_t)n * C + k], vb[k], s);
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) eff[n] = (pb ? pb[n] : 0.f) + s;
-  }
+  hvk_bias::attn_bias_fwd_body(blockIdx.x, gridDim.x, qb, vb, pb, w, C, qkv_bias, eff, dv_zero);
 }
 
-// 8 rows n of W per workgroup: d W[n, :] = g[n] v^T and the rows' share of d v = W^T g
-// (column partial sums, one f32 atomic per column per workgroup into d v, which the
-// forward launch zeroed)
-constexpr int kRows = 8;
-__global__ __launch_bounds__(256) void attn_bias_bwd_kernel(const float* __restrict__ g,
-                                                            const float* __restrict__ vb,
-                                                            const float* __restrict__ w, int C,
-                                                            float* __restrict__ dpb,
-                                                            float* __restrict__ dvb,
-                                                            float* __restrict__ dw) {
-  const int n0 = blockIdx.x * kRows;
-  for (int k = threadIdx.x; k < C; k += 256) {
-    const float vk = vb[k];
-    float acc = 0.f;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      const int n = n0 + r;
-      if (n < C) {
-        const float gn = g[n];
-        dw[(size_t)n * C + k] = gn * vk;
-        acc = fmaf(w[(size_t)n * C + k], gn, acc);
-      }
-    }
-    atomicAdd(dvb + k, acc);
-  }
-  if (dpb)
-    for (int i = threadIdx.x; i < kRows && n0 + i < C; i += 256) dpb[n0 + i] = g[n0 + i];
+constexpr int kRows = hvk_bias::kAbRows;
+__global__ __launch_bounds__(256) void attn_bias_bwd_kernel(const float* __restrict__ g, const float* __restrict__ vb,
+                                                            const float* __restrict__ w, int C, float* __restrict__ dpb,
+                                                            float* __restrict__ dvb, float* __restrict__ dw) {
+  hvk_bias::attn_bias_bwd_body(blockIdx.x, g, vb, w, C, dpb, dvb, dw);
 }
 
 }  // namespace

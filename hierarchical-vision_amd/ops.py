@@ -420,6 +420,72 @@ def cpb_table(coords, w1, b1, w2, logit_scale, clamp_max):
     return CpbTable.apply(coords, w1, b1, w2, logit_scale, clamp_max)
 
 
+class BlockTables(torch.autograd.Function):
+    """AttnBiasFn + CpbTable of one W-MSA block in one launch forward (hvk_block_bias_fwd)
+    and two backward (hvk_block_bias_bwd): (qkv GEMM bias, proj bias + W_proj v_bias, CPB
+    table [nH, RR], logit scale [nH]); same kernels' bodies, same results."""
+
+    @staticmethod
+    def forward(ctx, v_bias, proj_bias, proj_w, coords, w1, b1, w2, logit_scale, q_bias, clamp_max):
+        C = v_bias.numel()
+        v, pw = _f32(v_bias), _f32(proj_w)
+        pb = _f32(proj_bias) if proj_bias is not None else None
+        qb = _f32(q_bias.detach()) if q_bias is not None else None
+        coords, w1, b1, w2 = _f32(coords), _f32(w1), _f32(b1), _f32(w2)
+        logit = _f32(logit_scale.reshape(-1))
+        nH, hid = w2.shape
+        RR = coords.shape[0]
+        dev = v.device
+        qkv_bias = torch.empty(3 * C, device=dev, dtype=torch.float32)
+        eff = torch.empty(C, device=dev, dtype=torch.float32)
+        dv = torch.empty(C, device=dev, dtype=torch.float32)  # zeroed by the launch
+        table = torch.empty((nH, RR), device=dev, dtype=torch.float32)
+        scale = torch.empty(nH, device=dev, dtype=torch.float32)
+        call("hvk_block_bias_fwd", ptr(qb), ptr(v), ptr(pb), ptr(pw), C, ptr(coords), ptr(w1), ptr(b1),
+             ptr(w2), ptr(logit), float(clamp_max), RR, nH, hid, ptr(qkv_bias), ptr(eff), ptr(dv),
+             ptr(table), ptr(scale), stream())
+        ctx.save_for_backward(v, pw, coords, w1, b1, w2, logit, table)
+        ctx.dv = dv
+        ctx.has_pb = proj_bias is not None
+        ctx.clamp_max = float(clamp_max)
+        ctx.logit_shape = logit_scale.shape
+        ctx.mark_non_differentiable(qkv_bias)
+        ctx.set_materialize_grads(False)
+        return qkv_bias, eff, table, scale
+
+    @staticmethod
+    def backward(ctx, g_qkv, g_eff, dtable, dscale):
+        v, pw, coords, w1, b1, w2, logit, table = ctx.saved_tensors
+        C = v.numel()
+        nH, hid = w2.shape
+        RR = coords.shape[0]
+        dv, dpw, dpb = None, None, None
+        if g_eff is not None:
+            g_eff = _f32(g_eff)
+            dv, dpw = ctx.dv, torch.empty_like(pw)
+            dpb = torch.empty_like(g_eff) if ctx.has_pb else None
+        ctx.dv = None  # the returned d v_bias is then its only reference: AccumulateGrad steals it
+        dtable = _f32(dtable) if dtable is not None else torch.zeros_like(table)
+        dscale = _f32(dscale) if dscale is not None else torch.zeros_like(logit)
+        dw1, db1, dw2 = torch.empty_like(w1), torch.empty_like(b1), torch.empty_like(w2)
+        dlogit = torch.empty_like(logit)
+        nbytes = _lib.load().hvk_cpb_bwd_workspace_bytes(RR, nH)
+        key = (w1.device, nbytes)
+        ws = _CPB_WS.get(key)
+        if ws is None:
+            ws = _CPB_WS[key] = torch.empty(nbytes // 4, device=w1.device, dtype=torch.float32)
+        call("hvk_block_bias_bwd", ptr(g_eff), ptr(v), ptr(pw), C, ptr(dpb), ptr(dv), ptr(dpw),
+             ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), ctx.clamp_max, RR, nH, hid, ptr(table),
+             ptr(dtable), ptr(dscale), ptr(dw1), ptr(db1), ptr(dw2), ptr(dlogit), ptr(ws), nbytes,
+             stream())
+        return (dv, dpb, dpw, None, dw1, db1, dw2, dlogit.reshape(ctx.logit_shape), None, None)
+
+
+def block_tables(v_bias, proj_bias, proj_w, coords, w1, b1, w2, logit_scale, q_bias, clamp_max):
+    return BlockTables.apply(v_bias, proj_bias, proj_w, coords, w1, b1, w2, logit_scale, q_bias,
+                             clamp_max)
+
+
 # --------------------------------------------------------------------------- LayerNorm
 class LayerNormResidual(torch.autograd.Function):
     """x = x0 + s[b] * LayerNorm(a + abias); returns (x f32, x bf16 copy).  abias is the

@@ -221,13 +221,27 @@ class WindowAttention(nn.Module):
             return ops.attn_biases(self.q_bias, self.v_bias, self.proj.bias, self.proj.weight)
         return self.qkv_gemm_bias(), self.proj_bias()
 
+    def block_tables(self):
+        """(qkv GEMM bias, proj bias, CPB table, logit scale) = gemm_biases() + cpb_tables(),
+        on the GPU as one fused launch (ops.block_tables) when both fused forms apply."""
+        l1, l2 = self.cpb_mlp[0], self.cpb_mlp[2]
+        if (self.v_bias is not None and self.v_bias.is_cuda and _FUSED_TABLES
+                and isinstance(self.cpb_mlp[1], nn.ReLU) and l1.bias is not None and l2.bias is None
+                and l1.out_features == 512 and self.num_heads <= 32):
+            return ops.block_tables(self.v_bias, self.proj.bias, self.proj.weight,
+                                    self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias,
+                                    l2.weight, self.logit_scale, self.q_bias, self._logit_clamp)
+        return self.gemm_biases() + self.cpb_tables()
+
     def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None):
         """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] after proj (without
         proj's bias when proj_bias=False: the caller folds the proj bias into the next
-        kernel).  biases: gemm_biases() when the caller already has them."""
-        qkv_b, proj_b = biases if biases is not None else self.gemm_biases()
+        kernel).  biases: block_tables() (or gemm_biases()) when the caller already has them."""
+        if biases is None:
+            biases = self.block_tables()
+        qkv_b, proj_b = biases[:2]
         qkv = ops.linear(x, self.qkv.weight, qkv_b)
-        table, scale = self.cpb_tables()
+        table, scale = biases[2:] if len(biases) == 4 else self.cpb_tables()
         o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
                                       self.window_size[0], shift, q_bias=self.q_bias)
         return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None))
@@ -300,7 +314,7 @@ class SwinTransformerBlock(nn.Module):
         B, L, C = s.f32.shape
         assert L == H * W, "input feature has wrong size"
         fold = self.attn.proj_drop.p == 0 or not self.training  # proj bias -> LN kernel
-        biases = self.attn.gemm_biases()
+        biases = self.attn.block_tables()
         a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold,
                                      biases=biases)
         planned = getattr(self, "_dp", None) if self.training else None  # from _plan_drop_path
@@ -457,6 +471,9 @@ class PatchEmbed(nn.Module):
         Ho, Wo = self.patches_resolution
         f = Ho * Wo * self.embed_dim * self.in_chans * self.patch_size[0] * self.patch_size[1]
         return f + (Ho * Wo * self.embed_dim if self.norm is not None else 0)
+
+
+_FUSED_TABLES = os.environ.get("HVK_BLOCK_TABLES", "1") != "0"  # 0: separate launches (A/B runs)
 
 
 def _lib_ln_pool_ok(C):

@@ -172,6 +172,19 @@ int hvk_cpb_bwd(const float* coords, const float* w1, const float* b1, const flo
                 float* db1, float* dw2, float* dlogit, float* workspace, size_t workspace_bytes,
                 void* stream);
 
+/* One W-MSA block's small tables in one launch forward / two backward: hvk_attn_bias_fwd
+ * + hvk_cpb_fwd (same arguments and results), and hvk_attn_bias_bwd + hvk_cpb_bwd (g_eff
+ * NULL: the CPB part only).  Workspace: hvk_cpb_bwd_workspace_bytes(RR, nH). */
+int hvk_block_bias_fwd(const float* q_bias, const float* v_bias, const float* proj_bias, const float* proj_w,
+                       int C, const float* coords, const float* w1, const float* b1, const float* w2,
+                       const float* logit_scale, float clamp_max, int RR, int nH, int hidden, float* qkv_bias,
+                       float* eff, float* dv_zero, float* table, float* scale, void* stream);
+int hvk_block_bias_bwd(const float* g_eff, const float* v_bias, const float* proj_w, int C, float* d_proj_bias,
+                       float* d_v_bias, float* d_proj_w, const float* coords, const float* w1, const float* b1,
+                       const float* w2, const float* logit_scale, float clamp_max, int RR, int nH, int hidden,
+                       const float* table, const float* dtable, const float* dscale, float* dw1, float* db1,
+                       float* dw2, float* dlogit, float* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- Post-norm residual LayerNorm (with the producing Linear's bias folded in) -------
  * x = x0 + sample_scale[row / rows_per_sample] * LayerNorm(a + abias) (gamma, beta, eps)
  * Replaces swinv2.py:431 / 434 (shortcut + drop_path(norm(proj(x))) with proj/fc2 run

@@ -96,6 +96,37 @@ def test_patch_merge_gather_bit_exact():
     assert torch.equal(xg.grad, x)  # scatter is the exact inverse permutation
 
 
+@pytest.mark.parametrize("dim,heads,win", [(96, 3, 7), (768, 24, 7), (192, 6, 8)])
+def test_block_tables_match_separate_launches(dim, heads, win):
+    """ops.block_tables (one launch forward, two backward) == AttnBiasFn + CpbTable: the
+    four outputs and every parameter gradient (same kernel bodies; only the d v_bias atomics
+    may sum in another order)."""
+    import hvamd.swinv2 as sw
+    torch.manual_seed(dim)
+    m = sw.WindowAttention(dim, (win, win), heads).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    outs = {}
+    for fused in (True, False):
+        m.zero_grad(set_to_none=True)
+        if fused:
+            r = m.block_tables()
+        else:
+            r = m.gemm_biases() + m.cpb_tables()
+        torch.manual_seed(1)
+        g = [None] + [torch.randn_like(t) for t in r[1:]]
+        torch.autograd.backward([t for t in r[1:]], g[1:])
+        outs[fused] = ([t.detach().clone() for t in r],
+                       {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+    (ra, ga), (rb, gb) = outs[True], outs[False]
+    for a, b in zip(ra, rb):
+        assert torch.equal(a, b)
+    assert ga.keys() == gb.keys() and len(ga) >= 7, sorted(ga)
+    for n in ga:
+        assert torch.allclose(ga[n], gb[n], rtol=1e-6, atol=1e-6), n
+
+
 @pytest.mark.parametrize("B,T,C", [(256, 49, 768), (3, 5, 256), (2, 64, 1024), (4, 7, 1536)])
 def test_norm_pool_vs_torch(B, T, C):
     """Final LayerNorm + token mean (hvk_ln_pool_fwd / _bwd) vs torch f32 autograd of
