@@ -50,6 +50,10 @@ SIGNATURES = {
     "hvk_weight_grad_workspace": (_sz, [_i, _i, _i]),
     "hvk_weight_grad": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_gelu_in_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_gelu_in_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_weight_grad_gelu_x_supported": (_i, [_i, _i, _i]),
+    "hvk_weight_grad_gelu_x": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),

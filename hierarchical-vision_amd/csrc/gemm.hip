@@ -43,6 +43,8 @@ __device__ __forceinline__ int perm_row(int p) {
 // EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
 // bf16 pre-activation kept for the backward and the activation for fc2 (the reference's
 // F.linear(+bias) -> nn.GELU on the bf16 tensor, swinv2.py:58-62).
+// EPI 3 (fc2 forward on the saved pre-activation): Y = GELU(X) W^T (+ bias), the GELU of
+// each loaded X fragment recomputed and rounded to bf16 exactly as EPI 1 stores it.
 // EPI 2 (fc2 input gradient through the activation): Y = gh = bf16(acc * GELU'(h)) with h
 // read from Y2 (the saved fc1 pre-activation), and csum[n] += sum over rows of gh (the fc1
 // bias gradient): per-lane register sums over the workgroup's row tiles, one 16-lane
@@ -125,11 +127,14 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     hvk_f32x4 acc[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
+    uint4 xg[G::KS];  // EPI 3: the operand is GELU(X) (X = the saved fc1 pre-activation h)
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) xg[s] = EPI == 3 ? hvk_gelu8_bf16(xf[s]) : xf[s];
 #pragma unroll
     for (int s = 0; s < G::KS; ++s)
 #pragma unroll
       for (int t = 0; t < G::NT; ++t)
-        acc[t] = hvk_mfma16(wl[(t * G::U4 + 4 * s + g) * 16 + li], xf[s], acc[t]);
+        acc[t] = hvk_mfma16(wl[(t * G::U4 + 4 * s + g) * 16 + li], xg[s], acc[t]);
     const int row = 16 * tile + li;
     if (row < M) {
       hvk_bf16* yp = Y + (size_t)row * N + n0 + 8 * g;
@@ -330,6 +335,18 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   if (K == 96) return launch_linear<96, 384, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   if (K == 384) return launch_linear<384, 128, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+}
+
+int hvk_linear_gelu_in_supported(int M, int K, int N) { return M > 0 && K == 384 && N == 96; }
+
+int hvk_linear_gelu_in_fwd(const void* h, const void* w, const float* bias, void* y, int M, int K, int N,
+                           void* stream) {
+  if (!h || !w || !y) return hvk_set_error(HVK_EINVAL, "hvk_linear_gelu_in_fwd: null pointer");
+  if (!hvk_linear_gelu_in_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_gelu_in_fwd: shape M=%d K=%d N=%d not built", M, K, N);
+  return launch_linear<384, 96, 8, true, 3>(static_cast<const hvk_bf16*>(h), static_cast<const hvk_bf16*>(w),
+                                            bias, static_cast<hvk_bf16*>(y), M, N,
+                                            static_cast<hipStream_t>(stream));
 }
 
 int hvk_linear_gelu_bwd_supported(int M, int K, int N) {

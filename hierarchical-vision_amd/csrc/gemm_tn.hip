@@ -83,7 +83,7 @@ __device__ __forceinline__ void wait_stages(int r) {
   }
 }
 
-template <int FK, int FN, int WK, int WN, bool DB>
+template <int FK, int FN, int WK, int WN, bool DB, bool GX = false>
 __global__ __launch_bounds__(64 * WK * WN, 1) void dw_kernel(const hvk_bf16* __restrict__ G,
                                                            const hvk_bf16* __restrict__ X,
                                                            float* __restrict__ P, int N, int K,
@@ -178,7 +178,10 @@ __global__ __launch_bounds__(64 * WK * WN, 1) void dw_kernel(const hvk_bf16* __r
 #pragma unroll
     for (int b = 0; b < FN; ++b) fb[b] = tie2(rb[b][0], rb[b][1]);
 #pragma unroll
-    for (int a = 0; a < FK; ++a) fa[a] = tie2(ra[a][0], ra[a][1]);
+    for (int a = 0; a < FK; ++a) {
+      fa[a] = tie2(ra[a][0], ra[a][1]);
+      if (GX) fa[a] = hvk_gelu8_bf16(fa[a]);  // x = GELU(h) of the saved pre-activation
+    }
 #pragma unroll
     for (int a = 0; a < FK; ++a)
 #pragma unroll
@@ -278,7 +281,7 @@ bool plan(int M, int N, int K, Plan& p) {
   return true;
 }
 
-template <int FK, int FN, int WK, int WN>
+template <int FK, int FN, int WK, int WN, bool GX = false>
 int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, int K, const Plan& p,
            hipStream_t st) {
   using C = TnCfg<FK, FN, WK, WN>;
@@ -286,18 +289,18 @@ int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, 
   if (C::TK != p.tk || C::TN != p.tn) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad: plan/tile mismatch");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, true, GX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, false, GX>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
   const dim3 grid((unsigned)((p.ntiles * p.nchunk + 7) / 8 * 8));
   if (with_db)
-    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, true>), grid, dim3(C::THREADS), C::LDS, st, g, x, P,
+    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, true, GX>), grid, dim3(C::THREADS), C::LDS, st, g, x, P,
                        N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
   else
-    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, false>), grid, dim3(C::THREADS), C::LDS, st, g, x,
+    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, false, GX>), grid, dim3(C::THREADS), C::LDS, st, g, x,
                        P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
   HVK_CHECK_LAUNCH("hvk_weight_grad");
   return HVK_OK;
@@ -318,8 +321,8 @@ size_t hvk_weight_grad_workspace(int M, int N, int K) {
   return (size_t)p.nchunk * (size_t)p.pstride * sizeof(float);
 }
 
-int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
-                    size_t ws_bytes, void* stream) {
+static int weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
+                       size_t ws_bytes, void* stream, bool gx) {
   if (!g || !x || !dw || !ws) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad: null pointer");
   Plan p;
   if (!plan(M, N, K, p))
@@ -332,7 +335,10 @@ int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, i
   float* P = static_cast<float*>(ws);
   const bool wd = db != nullptr;
   int rc;
-  switch (p.var) {
+  if (gx && p.var != V_96x384)
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_weight_grad_gelu_x: M=%d N=%d K=%d", M, N, K);
+  switch (gx ? -1 : p.var) {
+    case -1: rc = launch<12, 3, 2, 2, true>(gb, xb, P, wd, N, K, p, st); break;
     case V_288x96: rc = launch<3, 9, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x96: rc = launch<3, 3, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_384x96: rc = launch<3, 12, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
@@ -350,6 +356,21 @@ int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, i
                      reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db));
   HVK_CHECK_LAUNCH("hvk_weight_grad_reduce");
   return HVK_OK;
+}
+
+int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
+                    size_t ws_bytes, void* stream) {
+  return weight_grad(g, x, dw, db, M, N, K, ws, ws_bytes, stream, false);
+}
+
+int hvk_weight_grad_gelu_x_supported(int M, int N, int K) {
+  Plan p;
+  return plan(M, N, K, p) && p.var == V_96x384 ? 1 : 0;
+}
+
+int hvk_weight_grad_gelu_x(const void* g, const void* h, float* dw, float* db, int M, int N, int K, void* ws,
+                           size_t ws_bytes, void* stream) {
+  return weight_grad(g, h, dw, db, M, N, K, ws, ws_bytes, stream, true);
 }
 
 }  // extern "C"

@@ -174,6 +174,20 @@ __device__ __forceinline__ f32x2 gelu_grad2(f32x2 u) {
 }
 }  // namespace hvk_gelu
 
+// GELU of 8 packed bf16 pre-activations, rounded back to bf16: the fc1 epilogue's stored
+// GELU(h), recomputed bit-identically where it is consumed instead of stored
+__device__ __forceinline__ uint4 hvk_gelu8_bf16(uint4 h) {
+  float u[8];
+  hvk_unpack8(h, u);
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const hvk_gelu::f32x2 y = hvk_gelu::gelu2(hvk_gelu::f32x2{u[e], u[e + 1]});
+    u[e] = y.x;
+    u[e + 1] = y.y;
+  }
+  return hvk_pack8(u);
+}
+
 // ---- MFMA 16x16x32 bf16 -> f32 --------------------------------------------
 // A lane l holds A[row l&15][k = 8(l>>4) + j], B lane l holds B[k = 8(l>>4) + j][col l&15],
 // D lane l holds D[row 4(l>>4) + r][col l&15], r = 0..3.

@@ -123,15 +123,38 @@ def _split_k_chunks(rows):
     return nc
 
 
-def weight_grad(g, x, with_db=False):
+# 1: keep only h and recompute GELU(h) in fc2 (off: measured slower)
+_GELU_RECOMPUTE = os.environ.get("HVK_GELU_RECOMPUTE", "0") == "1"
+
+
+def _gelu_recompute(M, K, N1, N2):
+    """With HVK_GELU_RECOMPUTE=1, MlpFn keeps only h = fc1(x) and recomputes GELU(h) inside
+    fc2's forward and weight gradient where both kernels are built (stage 0: K 96, N1 384,
+    N2 96).  Bit-identical results; off by default: on MI355X the recompute costs fc2 +80 µs
+    and its weight gradient +217 µs against the 233 µs the y write saves."""
+    lib = _lib.load()
+    return (_GELU_RECOMPUTE and _linear_native(M, K, N1) and lib.hvk_linear_gelu_in_supported(M, N1, N2)
+            and lib.hvk_weight_grad_gelu_x_supported(M, N2, N1))
+
+
+def weight_grad(g, x, with_db=False, gelu_x=False):
     """(dW, db) = (g^T x, g.sum(0)) in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to
     ~10^6): libhvk's token-chunked MFMA kernel with the bias gradient fused (hvk_weight_grad,
     one pass over g) for every SwinV2-T shape it is built for; otherwise the library GEMM
     batched over token chunks (thousands of workgroups) + a small sum.  db is None unless
-    with_db."""
+    with_db.  gelu_x: x holds the fc1 pre-activation h and the kernel contracts with GELU(h)
+    (hvk_weight_grad_gelu_x)."""
     M, N = g.shape
     K = x.shape[1]
     lib = _lib.load()
+    if gelu_x:  # x holds h; the kernel multiplies by GELU(h) (no fallback: callers check support)
+        dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
+        db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
+        nb = lib.hvk_weight_grad_workspace(M, N, K)
+        ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
+        call("hvk_weight_grad_gelu_x", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
+             ptr(ws), nb, stream())
+        return dw, db
     if lib.hvk_weight_grad_supported(M, N, K):
         dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
         db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
@@ -672,22 +695,39 @@ class MlpFn(torch.autograd.Function):
         w2b, w2t = _bf16_weight(w2)
         ctx.wts = (w1t, w2t)
         N1, K = w1b.shape
+        N2 = w2b.shape[0]
         x2 = xb.reshape(-1, K)
         M = x2.shape[0]
-        h, y1 = gelu_fwd(x2, w1b, b1)
-        y = mm_nt(y1, w2b, b2)
-        ctx.save_for_backward(xb, w1b, w2b, h, y1)
+        ctx.recompute = _gelu_recompute(M, K, N1, N2)
+        if ctx.recompute:
+            # GELU(h) is never stored: fc2 and its weight gradient recompute it per fragment
+            h = mm_nt(x2, w1b, b1)
+            y = torch.empty((M, N2), device=x2.device, dtype=torch.bfloat16)
+            b = _f32(b2) if b2 is not None else None
+            call("hvk_linear_gelu_in_fwd", ptr(h), ptr(w2b), ptr(b) if b is not None else None, ptr(y), M,
+                 N1, N2, stream())
+            ctx.save_for_backward(xb, w1b, w2b, h)
+        else:
+            h, y1 = gelu_fwd(x2, w1b, b1)
+            y = mm_nt(y1, w2b, b2)
+            ctx.save_for_backward(xb, w1b, w2b, h, y1)
         ctx.has_b2 = b2 is not None
-        return y.reshape(*xb.shape[:-1], w2b.shape[0])
+        return y.reshape(*xb.shape[:-1], N2)
 
     @staticmethod
     def backward(ctx, gy):
-        xb, w1b, w2b, h, y1 = ctx.saved_tensors
+        if ctx.recompute:
+            xb, w1b, w2b, h = ctx.saved_tensors
+        else:
+            xb, w1b, w2b, h, y1 = ctx.saved_tensors
         N1, K = w1b.shape
         N2 = w2b.shape[0]
         g2 = _bf16(gy).reshape(-1, N2)
         M = g2.shape[0]
-        dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
+        if ctx.recompute:
+            dw2, db2 = weight_grad(g2, h, ctx.has_b2, gelu_x=True)
+        else:
+            dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
         w2t = _bf16_t(w2b, ctx.wts[1])
         if _tile_ok(M, N2, N1):

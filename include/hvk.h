@@ -88,6 +88,12 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
  * dbias: f32 [N] or NULL, ACCUMULATED into (+= column sums of gh = the fc1 bias gradient;
  * the caller zeroes it).  Replaces the input-gradient GEMM + activation backward + bias reduction for
  * the (K, N) shapes hvk_linear_gelu_bwd_supported() reports. */
+/* fc2 forward on the saved pre-activation: y = GELU(h) w^T (+ bias), GELU recomputed per
+ * loaded fragment exactly as hvk_linear_gelu_fwd stores it (swinv2.py:58-65).  Built for
+ * K = 384, N = 96 (stage 0). */
+int hvk_linear_gelu_in_supported(int M, int K, int N);
+int hvk_linear_gelu_in_fwd(const void* h, const void* w, const float* bias, void* y, int M, int K, int N,
+                           void* stream);
 int hvk_linear_gelu_bwd_supported(int M, int K, int N);
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias, int M,
                         int K, int N, void* stream);
@@ -119,6 +125,12 @@ int hvk_weight_grad_supported(int M, int N, int K);
 size_t hvk_weight_grad_workspace(int M, int N, int K);
 int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
                     void* ws, size_t ws_bytes, void* stream);
+/* The same with x = GELU(h) recomputed from the saved bf16 fc1 pre-activation h (bit-identical
+ * to the stored GELU(h) of hvk_linear_gelu_fwd): fc2's weight gradient without GELU(h) kept
+ * in HBM.  Built for the stage-0 fc2 shape (N = 96, K = 384). */
+int hvk_weight_grad_gelu_x_supported(int M, int N, int K);
+int hvk_weight_grad_gelu_x(const void* g, const void* h, float* dw, float* db, int M, int N, int K, void* ws,
+                           size_t ws_bytes, void* stream);
 
 /* ---- bf16 weight copies for a step --------------------------------------------------
  * For k < n: dst[k] = bf16(src[k]) ([rows[k], cols[k]] row-major, f32 -> bf16 round to

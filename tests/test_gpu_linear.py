@@ -69,6 +69,32 @@ def test_linear_gelu_fused_matches_fp32(K, N):
         assert rel < 1e-2, (name, rel)
 
 
+@pytest.mark.parametrize("with_b2", [False, True])
+def test_mlp_gelu_recompute_bit_identical(monkeypatch, with_b2):
+    """Stage 0 MlpFn keeps only h and recomputes GELU(h) inside fc2's forward
+    (hvk_linear_gelu_in_fwd) and weight gradient (hvk_weight_grad_gelu_x): every output and
+    gradient equals the stored-GELU(h) path bit for bit."""
+    from hvamd import ops
+    M, C = 4096, 96
+    torch.manual_seed(3)
+    x0 = torch.randn(M, C, device="cuda").bfloat16()
+    w1 = torch.randn(4 * C, C, device="cuda") / C ** 0.5
+    b1 = torch.randn(4 * C, device="cuda")
+    w2 = torch.randn(C, 4 * C, device="cuda") / (4 * C) ** 0.5
+    b2 = torch.randn(C, device="cuda") if with_b2 else None
+    gy = torch.randn(M, C, device="cuda").bfloat16()
+    res = {}
+    for rec in (True, False):
+        monkeypatch.setattr(ops, "_GELU_RECOMPUTE", rec)
+        assert ops._gelu_recompute(M, C, 4 * C, C) == rec
+        ps = [t.clone().requires_grad_(True) if t is not None else None for t in (x0, w1, b1, w2, b2)]
+        y = ops.MlpFn.apply(*ps)
+        y.backward(gy)
+        res[rec] = [y.detach()] + [p.grad for p in ps if p is not None]
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("C", [96, 192, 384, 768])
 @pytest.mark.parametrize("with_b2", [False, True])
 def test_mlp_fused_backward_matches_fp32(C, with_b2):

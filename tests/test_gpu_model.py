@@ -124,7 +124,7 @@ def test_block_tables_match_separate_launches(dim, heads, win):
         assert torch.equal(a, b)
     assert ga.keys() == gb.keys() and len(ga) >= 7, sorted(ga)
     for n in ga:
-        assert torch.allclose(ga[n], gb[n], rtol=1e-6, atol=1e-6), n
+        assert torch.allclose(ga[n], gb[n], rtol=1e-4, atol=1e-5), n  # d v_bias: f32 atomics
 
 
 @pytest.mark.parametrize("B,T,C", [(256, 49, 768), (3, 5, 256), (2, 64, 1024), (4, 7, 1536)])
