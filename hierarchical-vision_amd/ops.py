@@ -188,19 +188,22 @@ def _linear_native(M, K, N):
 
 _TILE_ROUTE = int(os.environ.get("HVK_TILE_ROUTE", "1"))
 _TILE_S3 = int(os.environ.get("HVK_TILE_S3", "1"))
+_TILE_S1 = int(os.environ.get("HVK_TILE_S1", "1"))
 
 
 def _tile_ok(M, K, N):
     """libhvk's tiled MFMA GEMM (hvk_gemm_fwd) where it measured faster than the library GEMM
     (tools/bench_gemm.py): the stage-2 shapes (K <= 1536, fc2 forward and fc1 input gradient
-    included), the stage-1 N = 192 shapes with K = 576 / 768, and every stage-3 shape (and
-    the stage-2 PatchMerging) with 192 | N, on 128 x 192 tiles."""
+    included), the stage-1 shapes with 192 | N (K >= 192), and every stage-3 shape (and the
+    stage-2 PatchMerging) with 192 | N, on 128 x 192 tiles."""
     if K % 64 or M <= 0:
         return False
     if _TILE_ROUTE == 0:  # the earlier routing (A/B experiments): stage 2 with K <= 1152
         return not N % 128 and ((M >= 32768 and K <= 1152) or (K == 768 and N == 768))
-    if N % 128:  # the 128 x 192 tile: stage-1 fc2 forward and qkv / fc1 input gradients
-        return N == 192 and K in (576, 768) and M >= 32768
+    if N % 128:  # the 128 x 192 tile: stage-1 qkv / proj / fc2 forward, qkv / fc1 input grads
+        if not _TILE_S1:  # the narrower rule (A/B runs)
+            return N == 192 and K in (576, 768) and M >= 32768
+        return N % 192 == 0 and K >= 192 and M >= 32768
     if _TILE_S3 and M >= 8192 and N % 192 == 0:  # stage 3 and its PatchMerging (128 x 192 tiles)
         return True
     return (M >= 32768 and K <= 1536) or (K == 768 and N == 768)
