@@ -281,8 +281,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WmsaGeom& g = a.g;
   int chunk, h;
-  hvk_decode_chunk_head(blockIdx.x, g.nH, chunk, h);
-  if (chunk >= g.n_chunks) return;
+  if (!decode_item(g, blockIdx.x, chunk, h)) return;
   int w0, w1;
   chunk_range(g, chunk, w0, w1);
   if (w0 >= w1) return;
@@ -598,7 +597,8 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 
 template <int WIN>
 int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, hipStream_t st) {
-  const int padded = a.g.n_chunks;  // already a multiple of 8
+  const int items = a.g.n_chunks * a.g.nH;
+  const int nblk = a.g.xcd_runs ? 8 * ((items + 7) / 8) : (a.g.n_chunks + 7) / 8 * 8 * a.g.nH;
   const size_t lds = bwd_lds_bytes<WIN>();
   static bool attr_set = false;
   if (!attr_set) {
@@ -606,7 +606,7 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kernel<WIN>, dim3(padded * a.g.nH), dim3(kThreads), lds, st, a);
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kernel<WIN>, dim3(nblk), dim3(kThreads), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_bwd");
   hipLaunchKernelGGL(wmsa_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dbias_table,
                      dscale, dqb);
@@ -690,6 +690,19 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hvk_wmsa::large_window(window))
     return hvk_wmsa::large_bwd(a, window, dbias_table, dscale, dq_bias, st);
+  // fill all 256 CUs: 256 / nH chunks, not rounded down to a multiple of 8 (at 12 and 24 heads
+  // the rounding left 64 CUs idle), the (chunk, head) items dealt to the XCDs in runs of at
+  // most 32 (one resident workgroup per CU of each XCD)
+  static const bool fill = [] {
+    const char* e = getenv("HVK_WMSA_BWD_FILL");
+    return !e || atoi(e) != 0;
+  }();
+  if (fill) {
+    int c = 256 / num_heads;
+    if (c < 1) c = 1;
+    a.g.n_chunks = c < a.g.n_windows ? c : a.g.n_windows;
+    a.g.xcd_runs = 1;
+  }
   switch (window) {
     case 7: return launch_bwd<7>(a, dbias_table, dscale, dq_bias, st);
     case 8: return launch_bwd<8>(a, dbias_table, dscale, dq_bias, st);

@@ -8,7 +8,23 @@ struct WmsaGeom {
   int B, H, W, C, nH, shift;
   int nWh, nWw, n_windows;   // windows per image row/col, total windows (B*nWh*nWw)
   int n_chunks;              // window chunks per head (multiple of 8: XCD groups)
+  int xcd_runs;              // 1: (chunk, head) items dealt to the 8 XCDs in contiguous runs of
+                             //    ceil(items / 8) (any n_chunks), 0: hvk_decode_chunk_head
 };
+
+// workgroup -> (chunk, head); false for the padded grid's surplus workgroups
+__device__ __forceinline__ bool decode_item(const WmsaGeom& g, int bid, int& chunk, int& head) {
+  if (g.xcd_runs) {
+    const int items = g.n_chunks * g.nH, per = (items + 7) >> 3;
+    const int item = (bid & 7) * per + (bid >> 3);
+    if ((bid >> 3) >= per || item >= items) return false;
+    chunk = item / g.nH;
+    head = item % g.nH;
+    return true;
+  }
+  hvk_decode_chunk_head(bid, g.nH, chunk, head);
+  return chunk < g.n_chunks;
+}
 
 // token row (in the un-shifted [B*H*W] token order) of window position t
 __device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh, int ww, int win,
@@ -91,6 +107,7 @@ inline int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int
   if (chunks < 8) chunks = 8;
   const int need = (g.n_windows + 7) / 8 * 8;  // never more chunks than windows (rounded)
   g.n_chunks = chunks < need ? chunks : need;
+  g.xcd_runs = 0;
   return HVK_OK;
 }
 
