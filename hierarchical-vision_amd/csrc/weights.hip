@@ -51,6 +51,51 @@ __global__ __launch_bounds__(256) void cast_weights_kernel(CastBatch b) {
   }
 }
 
+// 64 x 64 tiles with 16-B loads and 8-B stores (rows and cols multiples of 4, every weight of
+// SwinV2): lane (ty, tx) of 16 x 16 handles rows ty + 16 i, columns 4 tx .. 4 tx + 3; the
+// transpose reads the LDS tile column-wise (stride 65 floats: conflict-free)
+__global__ __launch_bounds__(256) void cast_weights_v4_kernel(CastBatch b) {
+  __shared__ float tile[64][65];
+  const int bid = blockIdx.x;
+  int t = 0;
+  while (t + 1 < b.n && b.tile0[t + 1] <= bid) ++t;
+  const int local = bid - b.tile0[t];
+  const int R = b.rows[t], C = b.cols[t];
+  const int tc = (C + 63) >> 6;
+  const int r0 = (local / tc) * 64, c0 = (local % tc) * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const float* src = b.src[t];
+  hvk_bf16* dst = b.dst[t];
+  const int c = c0 + 4 * tx;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = r0 + ty + 16 * i;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < R && c < C) {
+      v = *reinterpret_cast<const float4*>(src + (size_t)r * C + c);
+      *reinterpret_cast<uint2*>(dst + (size_t)r * C + c) = make_uint2(hvk_pack2(v.x, v.y), hvk_pack2(v.z, v.w));
+    }
+    tile[ty + 16 * i][4 * tx] = v.x;
+    tile[ty + 16 * i][4 * tx + 1] = v.y;
+    tile[ty + 16 * i][4 * tx + 2] = v.z;
+    tile[ty + 16 * i][4 * tx + 3] = v.w;
+  }
+  hvk_bf16* dt = b.dst_t[t];
+  if (!dt) return;
+  __syncthreads();
+  const int rr = r0 + 4 * tx;  // 4 consecutive rows of W = 4 consecutive columns of W^T
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cc = c0 + ty + 16 * i;  // column of W = row of W^T
+    if (cc < C && rr < R) {
+      const int lr = ty + 16 * i;
+      *reinterpret_cast<uint2*>(dt + (size_t)cc * R + rr) =
+          make_uint2(hvk_pack2(tile[4 * tx][lr], tile[4 * tx + 1][lr]),
+                     hvk_pack2(tile[4 * tx + 2][lr], tile[4 * tx + 3][lr]));
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -63,6 +108,9 @@ int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* con
   for (int base = 0; base < n; base += kMaxT) {
     CastBatch b;
     b.n = n - base < kMaxT ? n - base : kMaxT;
+    bool v4 = true;  // every weight of the batch with rows and cols multiples of 4
+    for (int i = 0; i < b.n; ++i) v4 = v4 && rows[base + i] % 4 == 0 && cols[base + i] % 4 == 0;
+    const int T = v4 ? 64 : 32;
     int tiles = 0;
     for (int i = 0; i < b.n; ++i) {
       const int k = base + i;
@@ -74,10 +122,13 @@ int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* con
       b.rows[i] = rows[k];
       b.cols[i] = cols[k];
       b.tile0[i] = tiles;
-      tiles += ((rows[k] + 31) / 32) * ((cols[k] + 31) / 32);
+      tiles += ((rows[k] + T - 1) / T) * ((cols[k] + T - 1) / T);
     }
     b.tile0[b.n] = tiles;
-    hipLaunchKernelGGL(cast_weights_kernel, dim3(tiles), dim3(256), 0, st, b);
+    if (v4)
+      hipLaunchKernelGGL(cast_weights_v4_kernel, dim3(tiles), dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL(cast_weights_kernel, dim3(tiles), dim3(256), 0, st, b);
     HVK_CHECK_LAUNCH("hvk_cast_weights");
   }
   return HVK_OK;

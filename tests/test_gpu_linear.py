@@ -216,12 +216,15 @@ def test_gemm_tile_gelu_bwd_matches_fp32(M):
     assert (gh.float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
 
 
-def test_cast_weights_bit_exact_and_transposed():
+@pytest.mark.parametrize("shapes", [
+    [(288, 96), (96, 96), (33, 70), (1, 5), (768, 3072), (10, 1)],  # ragged: the 32 x 32 kernel
+    [(288, 96), (96, 96), (768, 3072), (10000, 768), (4, 4), (68, 132), (96, 48)],  # 4 | both: 64 x 64
+])
+def test_cast_weights_bit_exact_and_transposed(shapes):
     """hvk_cast_weights == weight.to(bfloat16) (round to nearest even) and its transpose, for
-    ragged shapes (not multiples of the 32 x 32 tile) in one launch."""
+    shapes that are not multiples of either kernel's tile, in one launch."""
     import ctypes
     from hvamd import _lib
-    shapes = [(288, 96), (96, 96), (33, 70), (1, 5), (768, 3072), (10, 1)]
     gen = torch.Generator(device="cuda").manual_seed(3)
     ws = [torch.randn(s, device="cuda", generator=gen) * 3 for s in shapes]
     dst = [torch.empty(s, device="cuda", dtype=torch.bfloat16) for s in shapes]
