@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  -- must be imported first: libhvk binds to torch's HIP runtime
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhvk.so")
+# HVK_LIB_PATH: another build of the same library (A/B runs of kernel variants, tools/gpu_ab_lib.sh)
+LIB_PATH = os.environ.get("HVK_LIB_PATH") or os.path.join(_HERE, "libhvk.so")
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int

@@ -196,6 +196,24 @@ __device__ __forceinline__ hvk_f32x4 hvk_mfma16(uint4 a, uint4 b, hvk_f32x4 c) {
                                                  __builtin_bit_cast(hvk_bf16x8, b), c, 0, 0, 0);
 }
 
+// MFMA result hazard across a branch.  hipcc (ROCm 7.2, gfx950) pads "an MFMA wrote v -> the next
+// instruction touching v" with 8 wait states inside a basic block, but NOT for a reader at a
+// taken-branch target when the MFMA ends the predecessor block: an unmasked W-MSA window that
+// branched over the mask code read its scores 2 states after the MFMA (wrong values, no fault).
+// hvk_settle(x, ...) after such MFMAs holds this wave 8 states in an asm statement that takes the
+// results as operands, so no reader can be scheduled above it (other waves issue meanwhile).
+// tools/mfma_hazard_audit.py walks every path of the built ISA and must report none.
+__device__ __forceinline__ void hvk_settle(hvk_f32x4& a) { asm volatile("s_nop 7" : "+v"(a)); }
+__device__ __forceinline__ void hvk_settle(hvk_f32x4& a, hvk_f32x4& b) {
+  asm volatile("s_nop 7" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void hvk_settle(hvk_f32x4& a, hvk_f32x4& b, hvk_f32x4& c) {
+  asm volatile("s_nop 7" : "+v"(a), "+v"(b), "+v"(c));
+}
+__device__ __forceinline__ void hvk_settle(hvk_f32x4& a, hvk_f32x4& b, hvk_f32x4& c, hvk_f32x4& d) {
+  asm volatile("s_nop 7" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, cols 4p..4p+3 of a
 // 4x16 bf16 block; lane i receives column i of the 4 rows (element q = row q).
 __device__ __forceinline__ uint2 hvk_tr_read(const hvk_bf16* lds) {

@@ -60,6 +60,13 @@ __device__ __forceinline__ PosInfo<WIN> key_info(int pos, int lim) {
   const int ph = pos / WIN, pw = pos - ph * WIN;
   return {ph * LCfg<WIN>::R + pw, ph >= lim, pw >= lim};
 }
+// the -100 shift-region mask of (key, query) as a select, not a branch on the (uniform) edge
+// flags: a branch over the mask code left its MFMA-result reader too close (hvk_common.h hvk_settle)
+template <int WIN>
+__device__ __forceinline__ float mask_of(bool edge_r, bool edge_c, const PosInfo<WIN>& k,
+                                         const PosInfo<WIN>& q, float mask2) {
+  return ((edge_r & (k.r != q.r)) | (edge_c & (k.c != q.c))) ? mask2 : 0.f;
+}
 
 // ------------------------------------------------------------------------------ forward
 template <int WIN>
@@ -102,7 +109,6 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
-  const bool edge = edge_r || edge_c;
 
   for (int t0 = wave * K::QB; t0 < K::NT; t0 += K::WAVES * K::QB) {
     uint4 qf[K::QB];
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float v = s[t][r] + tab[qi[j].b - ki[t][r].b];
-            if (edge && ((edge_r && ki[t][r].r != qi[j].r) || (edge_c && ki[t][r].c != qi[j].c))) v += mask2;
+            v += mask_of(edge_r, edge_c, ki[t][r], qi[j], mask2);
             if (kpad[t][r]) v = -INFINITY;
             s[t][r] = v;
             mc = fmaxf(mc, v);
@@ -252,7 +258,6 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
-  const bool edge = edge_r || edge_c;
 
   const float* bsrc = a.bias + (size_t)h * K::RR;
   for (int e = threadIdx.x; e < K::RR; e += K::THREADS) {
@@ -308,7 +313,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
           const int key = 16 * kt + 4 * gq + r;
           const PosInfo<WIN> ki = key_info<WIN>(key < K::N ? key : K::N - 1, lim);
           float x = s[r] + tab[qi.b - ki.b];
-          if (edge && ((edge_r && ki.r != qi.r) || (edge_c && ki.c != qi.c))) x += mask2;
+          x += mask_of(edge_r, edge_c, ki, qi, mask2);
           v[t][r] = key < K::N ? x : -INFINITY;
           dp[t][r] = d[r];
         }
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
           const PosInfo<WIN> ki = key_info<WIN>(kvalid ? key : K::N - 1, lim);
           const int idx = qi.b - ki.b;
           float x = s[r] + tab[idx];
-          if (edge && ((edge_r && ki.r != qi.r) || (edge_c && ki.c != qi.c))) x += mask2;
+          x += mask_of(edge_r, edge_c, ki, qi, mask2);
           const float p = kvalid ? __builtin_amdgcn_exp2f(x - lse) : 0.f;
           const float dsv = p * (d[r] - delta);
           ds[t][r] = dsv;
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
           const int q = 16 * qt + 4 * gq + r;
           const PosInfo<WIN> qi = query_info<WIN>(q < K::N ? q : K::N - 1, lim);
           float x = s[r] + tab[qi.b - ki.b];
-          if (edge && ((edge_r && ki.r != qi.r) || (edge_c && ki.c != qi.c))) x += mask2;
+          x += mask_of(edge_r, edge_c, ki, qi, mask2);
           p[t][r] = __builtin_amdgcn_exp2f(x - lr[r]);  // padding query: lse = +inf -> 0
           ds[t][r] = p[t][r] * (d[r] - dr[r]);
         }

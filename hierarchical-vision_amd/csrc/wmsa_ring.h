@@ -39,6 +39,19 @@ struct RingCfg {
   static constexpr int HI = BASE0 + LQMAX + TR * (NT - 1);       // largest index read
   static constexpr int TABF = ((PAD + (HI + 1 > R * R ? HI + 1 : R * R) + 3) / 4) * 4;
   static constexpr int LDS = SLAB + 16 + HG * TABF * 4;
+  // padding key slots (grid position x >= WIN or y >= WIN) of MFMA slot bit ki*4 + r for the
+  // lanes with lane/16 == gq, in bits 16*gq .. 16*gq + 15
+  static constexpr unsigned long long kpad_bits() {
+    unsigned long long v = 0;
+    for (int gq = 0; gq < 4; ++gq)
+      for (int ki = 0; ki < NT; ++ki)
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * ki + 4 * gq + r;
+          if (p % PW >= WIN || p / PW >= WIN) v |= 1ull << (16 * gq + ki * 4 + r);
+        }
+    return v;
+  }
+  static constexpr unsigned long long KPAD = kpad_bits();
   static_assert(NT <= 4, "window larger than 8 needs the large-window kernels");
 };
 
@@ -99,6 +112,16 @@ __device__ __forceinline__ void ring_bias_read_q(hvk_u32x2 (&br)[NT][2], uint32_
   if constexpr (NT > 1) if (qi == 1) ring_bias_read<TR, NT, (NT > 1 ? 1 : 0)>(br, a);
   if constexpr (NT > 2) if (qi == 2) ring_bias_read<TR, NT, (NT > 2 ? 2 : 0)>(br, a);
   if constexpr (NT > 3) if (qi == 3) ring_bias_read<TR, NT, (NT > 3 ? 3 : 0)>(br, a);
+}
+
+// hvk_settle over a query tile's NT score tiles (the unmasked-window path branches over the mask
+// code straight to the exp2 that reads them; hvk_common.h)
+template <int NT>
+__device__ __forceinline__ void settle_tiles(hvk_f32x4 (&s)[NT]) {
+  if constexpr (NT == 1) hvk_settle(s[0]);
+  if constexpr (NT == 2) hvk_settle(s[0], s[1]);
+  if constexpr (NT == 3) hvk_settle(s[0], s[1], s[2]);
+  if constexpr (NT == 4) hvk_settle(s[0], s[1], s[2], s[3]);
 }
 
 // padded-grid position -> window token (-1 for padding)

@@ -96,8 +96,14 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
   };
   // per-workgroup setup, overlapping nothing yet: bias tables = bias*log2e - M_h, where
   // M_h = scale*log2e + max(bias)*log2e bounds every logit of head h from above.  Softmax is
-  // shift invariant, so exp2 of the shifted logits needs no row max: each query's own key has
-  // cos = 1, so its shifted logit is >= -16*log2e and the row sum cannot underflow.
+  // shift invariant, so the fast path exponentiates these shifted logits without a row max.
+  // That is exact unless a query's best key lies far below the head bound (q and k come from
+  // different slices of qkv.weight, so max cos can be anywhere in [-1, 1]: at scale 100 a row
+  // with max cos < 0.3 can underflow to a zero row sum).  Every query tile therefore checks
+  // its row sums and, where any is below 2^-100, recomputes that tile with the true row max
+  // (the reference's softmax, swinv2.py:256): the fast path's result is kept only when it is
+  // provably accurate (every P entry is a bf16 with 8 mantissa bits at any exponent >= -126,
+  // so a row sum >= 2^-100 loses nothing that matters).
   // stored mirrored (entry PAD + i at TABF - 1 - PAD - i): the 4 accumulator rows r of a
   // (query tile, key tile) pair are then 4 ASCENDING dwords, read by two ds_read2_b32 straight
   // into the MFMA C operand
@@ -274,52 +280,118 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
     }
 #pragma unroll
     for (int qi = 0; qi < K::NT; ++qi) {
-      // one query tile live at a time, its bias reads inside the iteration (VGPR budget)
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      hvk_u32x2 br[K::NT][2];
-      ring_bias_read_q<K::TR, K::NT>(br, bta, qi);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      hvk_f32x4 s[K::NT];
-#pragma unroll
-      for (int ki = 0; ki < K::NT; ++ki) {
-        lds_fence(br[ki][0]);
-        lds_fence(br[ki][1]);
-        const hvk_f32x4 bb = {__uint_as_float(br[ki][0][0]), __uint_as_float(br[ki][0][1]),
-                              __uint_as_float(br[ki][1][0]), __uint_as_float(br[ki][1][1])};
-        s[ki] = hvk_mfma16(kf[ki], qf[qi], bb);
-      }
       const int pq = 16 * qi + li;
-      if (edge_r || edge_c) {  // wave-uniform: only the last window row / column is masked
-        const int qy = pq / K::PW, qx = pq % K::PW;
-        uint32_t mreg = 0;  // keys in another shift region than this query (swinv2.py:357-388)
-        if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
-        if (edge_c) mreg |= (kband >> 16) ^ (qx >= WIN - g.shift ? 0xFFFFu : 0u);
+      const int tq = grid_token<WIN, K::PW>(pq);
+      // S^T of query tile qi (shifted by the head bound) with the shift-region mask
+      auto scores = [&](hvk_f32x4 (&s)[K::NT]) {
+        // one query tile live at a time, its bias reads inside the iteration (VGPR budget)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        hvk_u32x2 br[K::NT][2];
+        ring_bias_read_q<K::TR, K::NT>(br, bta, qi);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int ki = 0; ki < K::NT; ++ki)
+        for (int ki = 0; ki < K::NT; ++ki) {
+          lds_fence(br[ki][0]);
+          lds_fence(br[ki][1]);
+          const hvk_f32x4 bb = {__uint_as_float(br[ki][0][0]), __uint_as_float(br[ki][0][1]),
+                                __uint_as_float(br[ki][1][0]), __uint_as_float(br[ki][1][1])};
+          s[ki] = hvk_mfma16(kf[ki], qf[qi], bb);
+        }
+        settle_tiles(s);
+        if (edge_r || edge_c) {  // wave-uniform: only the last window row / column is masked
+          const int qy = pq / K::PW, qx = pq % K::PW;
+          uint32_t mreg = 0;  // keys in another shift region than this query (swinv2.py:357-388)
+          if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
+          if (edge_c) mreg |= (kband >> 16) ^ (qx >= WIN - g.shift ? 0xFFFFu : 0u);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[ki][r] = fmaf((float)((mreg >> (ki * 4 + r)) & 1u), mask2, s[ki][r]);
-          }
-      }
-      // logits arrive shifted by the head bound M_h (bias table): no row max.  Padding keys
-      // hold finite logits here; their V rows and row-sum weights are zero.
+          for (int ki = 0; ki < K::NT; ++ki)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              s[ki][r] = fmaf((float)((mreg >> (ki * 4 + r)) & 1u), mask2, s[ki][r]);
+            }
+        }
+      };
+      // O^T = V^T P^T and the row sums of the (bf16) P over real keys
+      hvk_f32x4 o[2], osum;
+      auto pv = [&](const hvk_f32x4 (&s)[K::NT]) {
+        o[0] = o[1] = osum = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K::NC; ++c) {
+          const hvk_f32x4 a0 = s[2 * c];
+          const hvk_f32x4 a1 = (2 * c + 1 < K::NT) ? s[2 * c + 1] : hvk_f32x4{0, 0, 0, 0};
+          const uint4 pf = make_uint4(hvk_pack2(a0[0], a0[1]), hvk_pack2(a0[2], a0[3]),
+                                      hvk_pack2(a1[0], a1[1]), hvk_pack2(a1[2], a1[3]));
+          o[0] = hvk_mfma16(vt[c][0], pf, o[0]);
+          o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
+          osum = hvk_mfma16(ones[c], pf, osum);
+        }
+      };
+      hvk_f32x4 s[K::NT];
+      scores(s);
+      // fast path: exp2 of the head-bound-shifted logits, no row max.  Padding keys hold
+      // finite logits here; their V rows and row-sum weights are zero.
 #pragma unroll
       for (int ki = 0; ki < K::NT; ++ki)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(s[ki][r]);
-      hvk_f32x4 o[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, osum = {0, 0, 0, 0};
+      pv(s);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(tq >= 0 && !(osum[0] >= 0x1p-100f)) != 0, 0)) {
+        // slow path (rare, wave-uniform): the tile again with the true row max over real keys,
+        // one 16-key tile at a time (a second 16-register score array would spill): pass 1
+        // takes the max, pass 2 exponentiates against it and accumulates P V and the row sums
+        uint32_t mreg = 0;
+        if (edge_r || edge_c) {
+          const int qy = pq / K::PW, qx = pq % K::PW;
+          if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
+          if (edge_c) mreg |= (kband >> 16) ^ (qx >= WIN - g.shift ? 0xFFFFu : 0u);
+        }
+        // padding key slots of this lane (slot bit ki*4 + r) from a compile-time table indexed
+        // by gq: shifts, no compares (per-slot compare masks would be hoisted into SGPRs)
+        const uint32_t kpad = (uint32_t)(K::KPAD >> (16 * g4)) & 0xFFFFu;
+        auto tile = [&](int ki) {
+          const uint32_t ab = bta + 4 * K::TR * (K::NT - 1 - qi + ki);
+          hvk_u32x2 b0 = lds_rd2<0, 1>(ab), b1 = lds_rd2<2, 3>(ab);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          lds_fence(b0);
+          lds_fence(b1);
+          const hvk_f32x4 bb = {__uint_as_float(b0[0]), __uint_as_float(b0[1]), __uint_as_float(b1[0]),
+                                __uint_as_float(b1[1])};
+          hvk_f32x4 t = hvk_mfma16(kf[ki], qf[qi], bb);
 #pragma unroll
-      for (int c = 0; c < K::NC; ++c) {
-        const hvk_f32x4 a0 = s[2 * c];
-        const hvk_f32x4 a1 = (2 * c + 1 < K::NT) ? s[2 * c + 1] : hvk_f32x4{0, 0, 0, 0};
-        const uint4 pf = make_uint4(hvk_pack2(a0[0], a0[1]), hvk_pack2(a0[2], a0[3]),
-                                    hvk_pack2(a1[0], a1[1]), hvk_pack2(a1[2], a1[3]));
-        o[0] = hvk_mfma16(vt[c][0], pf, o[0]);
-        o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
-        osum = hvk_mfma16(ones[c], pf, osum);  // row sums of the (bf16) P over real keys
+          for (int r = 0; r < 4; ++r) {
+            t[r] = fmaf((float)((mreg >> (ki * 4 + r)) & 1u), mask2, t[r]);
+            t[r] = fmaf((float)((kpad >> (ki * 4 + r)) & 1u), -1e30f, t[r]);  // padding: weight 0
+          }
+          return t;
+        };
+        float m = -INFINITY;
+#pragma unroll
+        for (int ki = 0; ki < K::NT; ++ki) {
+          const hvk_f32x4 t = tile(ki);
+          m = fmaxf(m, fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3])));
+        }
+        m = fmaxf(m, __shfl_xor(m, 16));  // the 4 lanes (gq) holding one query's keys
+        m = fmaxf(m, __shfl_xor(m, 32));
+        o[0] = o[1] = osum = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < K::NC; ++c) {
+          hvk_f32x4 a0 = tile(2 * c), a1 = {0, 0, 0, 0};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a0[r] = __builtin_amdgcn_exp2f(a0[r] - m);
+          if (2 * c + 1 < K::NT) {  // else the chunk's upper 16 keys do not exist: P = 0
+            a1 = tile(2 * c + 1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a1[r] = __builtin_amdgcn_exp2f(a1[r] - m);
+          }
+          const uint4 pf = make_uint4(hvk_pack2(a0[0], a0[1]), hvk_pack2(a0[2], a0[3]),
+                                      hvk_pack2(a1[0], a1[1]), hvk_pack2(a1[2], a1[3]));
+          o[0] = hvk_mfma16(vt[c][0], pf, o[0]);
+          o[1] = hvk_mfma16(vt[c][1], pf, o[1]);
+          osum = hvk_mfma16(ones[c], pf, osum);
+        }
+        hvk_settle(o[0], o[1], osum);  // read by the store block the slow path branches back to
       }
-      const int tq = grid_token<WIN, K::PW>(pq);
       if (tq >= 0) {
         const float inv = __builtin_amdgcn_rcpf(osum[0]);
         const uint4 v = make_uint4(hvk_pack2(o[0][0] * inv, o[0][1] * inv),

@@ -69,6 +69,64 @@ def test_wmsa_backward_matches_oracle(B, H, W, nh, win, shift):
         assert rel < (5e-2 if name == "dscale" else 2e-2), (name, rel)
 
 
+def _anti_aligned(B, H, W, nh, win, seed, noise):
+    """q = -u + noise, k = u + noise per (token, head) with v random, scale 100 (logit_scale at
+    its ln 100 clamp, swinv2.py:138): every cos(q_i, k_j) is near -1, so each row's best logit
+    sits ~2 * 100 nats below the per-head bound scale + max bias (the ring forward's fast-path
+    shift) and a softmax without a row max underflows to 0 / 0."""
+    rng = np.random.default_rng(seed)
+    C = 32 * nh
+    u = rng.standard_normal((B, H * W, C))
+    q = -u + noise * rng.standard_normal((B, H * W, C))
+    k = u + noise * rng.standard_normal((B, H * W, C))
+    v = rng.standard_normal((B, H * W, C))
+    qkv = torch.from_numpy(np.concatenate([q, k, v], -1).astype(np.float32)).bfloat16().float()
+    tab = torch.from_numpy((16 / (1 + np.exp(-rng.standard_normal((nh, (2 * win - 1) ** 2))))).astype(np.float32))
+    return qkv, tab, torch.full((nh,), 100.0)
+
+
+LARGE_SCALE_CASES = [  # ring kernels (w <= 8) incl. shifted edge windows, and the large-window form
+    (2, 14, 14, 2, 7, 3), (1, 28, 28, 6, 7, 3), (2, 7, 7, 4, 7, 0), (1, 16, 16, 2, 8, 4),
+    (1, 12, 12, 3, 6, 3), (1, 8, 8, 2, 4, 2), (1, 24, 24, 2, 12, 6), (1, 48, 48, 2, 24, 12),
+]
+
+
+@pytest.mark.parametrize("noise", [0.0, 0.3])
+@pytest.mark.parametrize("B,H,W,nh,win,shift", LARGE_SCALE_CASES)
+def test_wmsa_scale100_anti_aligned_matches_oracle(B, H, W, nh, win, shift, noise):
+    """The forward must keep the reference's softmax (row max, swinv2.py:256) where the
+    head-bound shift alone underflows: finite outputs equal to the oracle's, and finite
+    gradients equal to the oracle's."""
+    import hvamd.ops as ops
+    qkv, tab, scale = _anti_aligned(B, H, W, nh, win, 11, noise)
+    ref = swinv2_ref.wmsa_core_ref(qkv, tab, scale, H, W, nh, win, shift)
+    q_gpu = qkv.cuda().bfloat16().requires_grad_(True)
+    t_gpu = tab.cuda().requires_grad_(True)
+    s_gpu = scale.cuda().requires_grad_(True)
+    out = ops.window_attention_core(q_gpu, t_gpu, s_gpu, H, W, nh, win, shift)
+    o = out.float().cpu()
+    assert torch.isfinite(o).all()
+    rel = ((o - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+    gout = torch.from_numpy(np.random.default_rng(5).standard_normal(o.shape).astype(np.float32))
+    gout = gout.bfloat16().float()
+    q_ref, t_ref, s_ref = (x.clone().requires_grad_(True) for x in (qkv, tab, scale))
+    swinv2_ref.wmsa_core_ref(q_ref, t_ref, s_ref, H, W, nh, win, shift).backward(gout)
+    out.backward(gout.cuda().bfloat16())
+    torch.cuda.synchronize()
+    for name, mine, r in [("dqkv", q_gpu.grad, q_ref.grad), ("dbias", t_gpu.grad, t_ref.grad),
+                          ("dscale", s_gpu.grad, s_ref.grad)]:
+        mine = mine.float().cpu()
+        assert torch.isfinite(mine).all(), name
+        if name == "dscale" and noise == 0.0:
+            # every cos is -1 up to bf16 rounding: d scale = sum(dS * cos) = -sum(dS) ~ 0 (rows
+            # of dS sum to 0), so only an absolute bound is meaningful
+            assert (mine - r).abs().max().item() < 5e-2 * r.abs().max().item() + 1e-2, (mine, r)
+            continue
+        rel = ((mine - r).norm() / r.norm().clamp_min(1e-12)).item()
+        assert rel < (5e-2 if name == "dscale" else 2e-2), (name, rel)
+
+
 def test_wmsa_rejects_unsupported_head_dim():
     import hvamd.ops as ops
     qkv = torch.zeros(1, 49, 3 * 48, device="cuda", dtype=torch.bfloat16)
