@@ -5,6 +5,10 @@ taxonomy, one data-parallel training step per "step", 256 images per GPU
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself
+(torch.distributed.run on 127.0.0.1 as a child process, before anything touches the GPU) and
+exits with its status; under an external launcher WORLD_SIZE must equal --gpus.
+
 A step = forward + HXE loss + backward (bucketed RCCL all-reduce overlapped) + grad-norm
 clip + DecoupledSGDW update, bf16 autocast, f32 master weights; synthetic images/labels
 resident in HBM.  Rank 0 prints one JSON line.  The W-MSA roofline is measured live with
@@ -43,6 +47,9 @@ def parse():
     ap.add_argument("--graph", type=int, default=0,
                     help="1: time HIP-graph replays of the step (trainer.capture/replay); 0: eager "
                          "(default: keeps the RCCL all-reduce overlapped with the backward)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the measured path); gloo only to rehearse the "
+                         "multi-rank flow with several ranks sharing one GPU")
     ap.add_argument("--roofline-steps", type=int, default=4,
                     help="graph mode: eager warm-up steps whose W-MSA launches are timed")
     return ap.parse_args()
@@ -156,15 +163,41 @@ def cpu_baseline(args, seconds):
             "sample": f"{n} train steps x {bs} images (SwinV2-T 224 + HXE, f32, oracle/swinv2_ref.py)"}
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run as a child
+    (one process per GPU, RCCL rendezvous on 127.0.0.1) and return its exit status.  Nothing
+    here touches the GPU, so the parent holds no device context while the ranks run."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share a GPU
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise RuntimeError(f"RCCL sees {dist.get_world_size()} ranks, expected {world}")
     import hvamd.ops as ops
 
     cfg, tax, model, trainer = build(args, device)
@@ -230,6 +263,10 @@ def main():
                    "parallelism": f"dp{world}",
                    "execution": "hip-graph replay" if args.graph else "eager"},
         "value_per_gpu": round(value / world, 2),
+        "comm": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                  "grad_buckets": len(trainer.buckets.buckets),
+                  "grad_bytes_per_step": 4 * sum(b[0].numel() for b in trainer.buckets.buckets)}
+                 if world > 1 else None),
         "final_loss": round(loss_val, 4),
     }
     if timer:

@@ -47,7 +47,8 @@ SIGNATURES = {
     "hvk_attn_bias_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "hvk_attn_bias_bwd": (_i, [_p, _p, _p, _i, _p, _p, _p, _p]),
     "hvk_sgdw_workspace_bytes": (_sz, [_i, _p]),
-    "hvk_sgdw_step": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _i, _f, _f, _f, _i, _i, _p, _sz, _p]),
+    "hvk_sgdw_step": (_i, [_i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _p, _f, _f, _f, _f, _i, _i, _f, _p, _sz,
+                           _p]),
     "hvk_weight_grad_workspace": (_sz, [_i, _i, _i]),
     "hvk_weight_grad": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),

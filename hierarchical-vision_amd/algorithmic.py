@@ -121,7 +121,12 @@ class GradientClipping(Algorithm):
 
 class EMA(Algorithm):
     """Exponential moving average of the weights every `update_interval` batches with
-    smoothing from a half-life in batches (configs/pretrain/inat21.yaml:32-35)."""
+    smoothing from a half-life in batches (configs/pretrain/inat21.yaml:32-35).
+
+    On an update batch the average is handed to an optimizer that can fold it into its own
+    pass over the weights (optim.DecoupledSGDW's fused step: ema = a ema + (1 - a) p with the
+    freshly updated p, so the weights are not read again); otherwise, and in HIP-graph replays
+    (the captured update runs every step), it runs as foreach passes at BATCH_END."""
 
     def __init__(self, half_life="100ba", update_interval="20ba", smoothing=None):
         hl = int(str(half_life).rstrip("ba"))
@@ -129,17 +134,35 @@ class EMA(Algorithm):
         self.smoothing = smoothing if smoothing is not None else math.exp(
             -math.log(2) * self.update_interval / hl)
         self.ema_params = None
+        self._handed = False
 
     def match(self, event, state):
-        return event == Event.BATCH_END
+        return event in (Event.AFTER_BACKWARD, Event.BATCH_END)
 
     @torch.no_grad()
     def apply(self, event, state, logger=None):
         params = [p for p in state.model.parameters()]
+        if event == Event.AFTER_BACKWARD:
+            self._handed = False
+            if self.ema_params is None or (state.timestamp_batch + 1) % self.update_interval:
+                return
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                return
+            opts = getattr(state, "optimizers", None) or []
+            opt = opts[0] if len(opts) == 1 else None
+            if (opt is not None and all(p.grad is not None for p in params)
+                    and getattr(opt, "supports_fused_ema", lambda ps: False)(params)):
+                opt.pending_ema = ([(id(p), e) for p, e in zip(params, self.ema_params)],
+                                   self.smoothing)
+                self._handed = True
+            return
         if self.ema_params is None:
             self.ema_params = [p.detach().clone() for p in params]
             return
         if state.timestamp_batch % self.update_interval:
+            return
+        if self._handed:  # folded into this step's optimizer pass
+            self._handed = False
             return
         torch._foreach_mul_(self.ema_params, self.smoothing)
         torch._foreach_add_(self.ema_params, [p.detach() for p in params], alpha=1 - self.smoothing)

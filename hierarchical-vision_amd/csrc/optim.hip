@@ -1,16 +1,21 @@
-// Fused optimizer step for the training loop: global-norm gradient clipping
-// (torch.nn.utils.clip_grad_norm_, algorithmic.py GradientClipping -> composer) and
-// DecoupledSGDW (composer.optim.DecoupledSGDW: momentum SGD with weight decay decoupled
-// from the gradient, scaled by lr / initial_lr) over every parameter tensor in three
-// launches, instead of one foreach pass per operation:
+// Fused optimizer step for the training loop: the data-parallel gradient mean, global-norm
+// gradient clipping (torch.nn.utils.clip_grad_norm_, algorithmic.py GradientClipping ->
+// composer), DecoupledSGDW (composer.optim.DecoupledSGDW: momentum SGD with weight decay
+// decoupled from the gradient, scaled by lr / initial_lr) and, on the batches the recipe asks
+// for it, the weight EMA (configs/pretrain/inat21.yaml:31-34) over every parameter tensor in
+// three launches, instead of one foreach pass per operation:
 //   1. sumsq: each workgroup writes the sum of squares of its gradient chunk to its slot of
 //      the workspace (no atomics, no memset);
 //   2. coef: one workgroup sums the slots (fixed order: deterministic) and stores
-//      coef = min(1, max_norm / (||g|| + 1e-6));
+//      coef = s min(1, max_norm / (s ||g|| + 1e-6)) with s = grad_scale (1 / world for the
+//      summed all-reduce buckets: the mean is never materialised as a separate pass);
 //   3. update, per chunk:
 //        g' = coef g;  m = first ? g' : mom m + (1 - damp) g';  u = nesterov ? g' + mom m : m
 //        p = p * decay - lr u      (decay = 1 - wd lr / initial_lr, 1 for the no-decay group)
+//        ema = a ema + (1 - a) p   (only with an EMA table: the new p is in registers already)
 //      with the products rounded in the same order as the torch foreach sequence.
+// lr / decay come from the kernel arguments or, for HIP-graph replays (trainer.py), from a
+// device array the host refreshes before each replay.
 // The tensor table (pointers, sizes, parameter group) travels in the kernel arguments, up to
 // kBatch tensors per launch (no device-side table to keep in sync with the autograd-owned
 // gradient buffers, and graph capture sees plain kernel nodes).
@@ -23,12 +28,13 @@ namespace {
 constexpr int kChunk = 16384;  // elements per workgroup
 constexpr int kThreads = 256;
 constexpr int kMaxGroups = 4;
-constexpr int kBatch = 80;
+constexpr int kBatch = 64;  // 48-B entries: the table stays well inside the kernel-argument limit
 
 struct Entry {  // one parameter tensor
   float* p;
   const float* g;
   float* m;
+  float* ema;  // nullptr: no EMA this step
   int n;
   int chunk0;  // first chunk of the tensor (within its batch)
   int group;   // parameter group; bit 8: pointers 16-B aligned and n % 4 == 0
@@ -90,12 +96,12 @@ __global__ __launch_bounds__(kThreads) void sumsq_kernel(Batch b, float* __restr
 }
 
 __global__ __launch_bounds__(kThreads) void coef_kernel(float* __restrict__ part, int nparts,
-                                                       float max_norm) {
+                                                       float max_norm, float gscale) {
   __shared__ float red[kThreads / 64];
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += kThreads) s += part[i];
   s = block_sum(s, red);
-  if (threadIdx.x == 0) part[nparts] = fminf(1.f, max_norm / (sqrtf(s) + 1e-6f));
+  if (threadIdx.x == 0) part[nparts] = gscale * fminf(1.f, max_norm / (gscale * sqrtf(s) + 1e-6f));
 }
 
 __device__ __forceinline__ void sgdw1(float& p, float& m, float g, float coef, float mom, float damp,
@@ -107,12 +113,20 @@ __device__ __forceinline__ void sgdw1(float& p, float& m, float g, float coef, f
   p = fmaf(-lr, u, __fmul_rn(p, decay));
 }
 
+__device__ __forceinline__ void ema1(float& e, float p, float a) {
+  e = fmaf(1.f - a, p, __fmul_rn(e, a));
+}
+
 __global__ __launch_bounds__(kThreads) void sgdw_kernel(Batch b, const float* __restrict__ coefp,
-                                                       Groups grp, float mom, float damp,
-                                                       int nesterov, int first) {
+                                                       float coef_host, Groups grp,
+                                                       const float* __restrict__ hyper, float mom,
+                                                       float damp, int nesterov, int first,
+                                                       float ema_a) {
   const Entry e = b.e[find_entry(b.e, b.nt, blockIdx.x)];
-  const float coef = coefp ? *coefp : 1.f;
-  const float decay = grp.decay[e.group & 255], lr = grp.lr[e.group & 255];
+  const float coef = coefp ? *coefp : coef_host;
+  const int gi = e.group & 255;
+  const float decay = hyper ? hyper[kMaxGroups + gi] : grp.decay[gi];
+  const float lr = hyper ? hyper[gi] : grp.lr[gi];
   const long long c0 = (long long)(blockIdx.x - e.chunk0) * kChunk;
   const long long c1 = c0 + kChunk < e.n ? c0 + kChunk : e.n;
   const bool nes = nesterov != 0, fst = first != 0;
@@ -130,6 +144,12 @@ __global__ __launch_bounds__(kThreads) void sgdw_kernel(Batch b, const float* __
       sgdw1(p.w, m.w, g.w, coef, mom, damp, nes, fst, decay, lr);
       p4[i] = p;
       m4[i] = m;
+      if (e.ema) {
+        float4* e4 = reinterpret_cast<float4*>(e.ema);
+        float4 q = e4[i];
+        ema1(q.x, p.x, ema_a); ema1(q.y, p.y, ema_a); ema1(q.z, p.z, ema_a); ema1(q.w, p.w, ema_a);
+        e4[i] = q;
+      }
     }
   } else {
     for (long long i = c0 + threadIdx.x; i < c1; i += kThreads) {
@@ -137,6 +157,7 @@ __global__ __launch_bounds__(kThreads) void sgdw_kernel(Batch b, const float* __
       sgdw1(p, m, e.g[i], coef, mom, damp, nes, fst, decay, lr);
       e.p[i] = p;
       e.m[i] = m;
+      if (e.ema) ema1(e.ema[i], p, ema_a);
     }
   }
 }
@@ -154,12 +175,15 @@ size_t hvk_sgdw_workspace_bytes(int n, const long long* numel) {
 }
 
 int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m,
-                  const long long* numel, const int* group, const float* lr, const float* decay,
-                  int ngroups, float max_norm, float momentum, float dampening, int nesterov,
-                  int first, float* workspace, size_t ws_bytes, void* stream) {
+                  float* const* ema, const long long* numel, const int* group, const float* lr,
+                  const float* decay, int ngroups, const float* hyper, float grad_scale,
+                  float max_norm, float momentum, float dampening, int nesterov, int first,
+                  float ema_smoothing, float* workspace, size_t ws_bytes, void* stream) {
   if (n <= 0) return HVK_OK;
   if (!p || !g || !m || !numel || !group || !lr || !decay || !workspace)
     return hvk_set_error(HVK_EINVAL, "hvk_sgdw_step: null argument");
+  if (!(grad_scale > 0.f))
+    return hvk_set_error(HVK_EINVAL, "hvk_sgdw_step: grad_scale %g", (double)grad_scale);
   if (ngroups < 1 || ngroups > kMaxGroups)
     return hvk_set_error(HVK_EINVAL, "hvk_sgdw_step: %d parameter groups (max %d)", ngroups, kMaxGroups);
   if (ws_bytes < hvk_sgdw_workspace_bytes(n, numel))
@@ -174,12 +198,14 @@ int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m
     int ch = 0;
     for (int i = 0; i < b.nt; ++i) {
       const int k = (int)bi * kBatch + i;
-      if (!p[k] || !g[k] || !m[k] || numel[k] <= 0 || numel[k] > (1ll << 30) || group[k] < 0 ||
-          group[k] >= ngroups)
+      float* ek = ema ? ema[k] : nullptr;
+      if (!p[k] || !g[k] || !m[k] || (ema && !ek) || numel[k] <= 0 || numel[k] > (1ll << 30) ||
+          group[k] < 0 || group[k] >= ngroups)
         return hvk_set_error(HVK_EINVAL, "hvk_sgdw_step: tensor %d invalid", k);
       const bool v4 = ((reinterpret_cast<size_t>(p[k]) | reinterpret_cast<size_t>(g[k]) |
-                        reinterpret_cast<size_t>(m[k])) % 16 == 0) && numel[k] % 4 == 0;
-      b.e[i] = Entry{p[k], g[k], m[k], (int)numel[k], ch, group[k] | (v4 ? 256 : 0)};
+                        reinterpret_cast<size_t>(m[k]) | reinterpret_cast<size_t>(ek)) % 16 == 0) &&
+                      numel[k] % 4 == 0;
+      b.e[i] = Entry{p[k], g[k], m[k], ek, (int)numel[k], ch, group[k] | (v4 ? 256 : 0)};
       ch += chunks_of(numel[k]);
     }
     part += ch;
@@ -196,13 +222,14 @@ int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m
       hipLaunchKernelGGL(sumsq_kernel, dim3(nch(b)), dim3(kThreads), 0, st, b, workspace);
       HVK_CHECK_LAUNCH("hvk_sgdw_step (norm)");
     }
-    hipLaunchKernelGGL(coef_kernel, dim3(1), dim3(kThreads), 0, st, workspace, part, max_norm);
+    hipLaunchKernelGGL(coef_kernel, dim3(1), dim3(kThreads), 0, st, workspace, part, max_norm,
+                       grad_scale);
     HVK_CHECK_LAUNCH("hvk_sgdw_step (coef)");
     coefp = workspace + part;
   }
   for (const Batch& b : batches) {
-    hipLaunchKernelGGL(sgdw_kernel, dim3(nch(b)), dim3(kThreads), 0, st, b, coefp, gp, momentum,
-                       dampening, nesterov, first);
+    hipLaunchKernelGGL(sgdw_kernel, dim3(nch(b)), dim3(kThreads), 0, st, b, coefp, grad_scale, gp,
+                       hyper, momentum, dampening, nesterov, first, ema_smoothing);
     HVK_CHECK_LAUNCH("hvk_sgdw_step");
   }
   return HVK_OK;

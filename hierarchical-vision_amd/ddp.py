@@ -13,7 +13,9 @@ Design for MI355X:
   64 MB): xGMI is point-to-point (7 links/GPU) and RCCL's ring/tree per-call
   cost is amortised only by large messages.
 * ``synchronize()`` waits for all buckets (makes the current stream wait on the
-  RCCL stream, no host sync) and applies the 1/world mean.
+  RCCL stream, no host sync).  The 1/world mean is not a separate pass over the 141 MB: the
+  trainer hands it to the fused optimizer step as a gradient scale (optim.DecoupledSGDW);
+  ``synchronize(scale=True)`` divides in place for optimizers that cannot take it.
 No other collective runs in the step.
 """
 import torch
@@ -87,8 +89,9 @@ class GradientBuckets:
                     raise RuntimeError("param.grad was detached from its bucket; "
                                        "use zero_grad(set_to_none=False) or buckets.reset()")
 
-    def synchronize(self):
-        """Wait for every bucket's all-reduce and turn sums into means."""
+    def synchronize(self, scale=True):
+        """Wait for every bucket's all-reduce; with scale, turn the sums into means in place
+        (scale=False leaves sums for an optimizer that applies 1/world itself)."""
         if not self.enabled:
             return
         for i, (flat, _) in enumerate(self.buckets):
@@ -96,7 +99,8 @@ class GradientBuckets:
             if w is None:  # a bucket whose grads never arrived (unused params): reduce now
                 w = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             w.wait()
-            flat.div_(self.world)
+            if scale:
+                flat.div_(self.world)
 
     def zero_(self):
         """Zero the buckets in place (graph mode: captured at the start of the backward graph)."""

@@ -24,7 +24,14 @@ def set_weight_decay(model, skip_list=()):
 
 class DecoupledSGDW(torch.optim.Optimizer):
     """SGD + momentum with weight decay decoupled from the gradient and scaled by
-    lr / initial_lr (composer.optim.DecoupledSGDW semantics), foreach kernels."""
+    lr / initial_lr (composer.optim.DecoupledSGDW semantics).
+
+    On the GPU one step is libhvk's fused hvk_sgdw_step (include/hvk.h), which also takes the
+    hand-overs of the step's other per-parameter passes so none of them reads the 141 MB of
+    gradients or weights again: ``pending_grad_scale`` (1/world: the DDP buckets hold gradient
+    SUMS, ddp.py), ``pending_clip`` (GradientClipping's norm threshold) and ``pending_ema``
+    (the EMA algorithm's averaged copies on the batches it updates them).  Elsewhere the same
+    step runs as foreach passes."""
 
     def __init__(self, params, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
@@ -32,10 +39,23 @@ class DecoupledSGDW(torch.optim.Optimizer):
         super().__init__(params, defaults)
 
         self.pending_clip = None  # global-norm threshold handed over by GradientClipping
+        self.pending_grad_scale = 1.0  # gradient multiplier handed over by the trainer (DDP mean)
+        self.pending_ema = None  # ([(id(param), ema tensor)], smoothing) from the EMA algorithm
+        self.device_hyper = False  # graph mode: lr / decay read from a device array at run time
+        self._hyper = None
         self._fused = None
 
     def supports_fused_clip(self):
         return True
+
+    def supports_grad_scale(self):
+        return True
+
+    def supports_fused_ema(self, params):
+        """The fused step can apply an EMA over exactly these parameters when every one of them
+        is in a param group (the trainer asks before handing the EMA over)."""
+        mine = {id(p) for g in self.param_groups for p in g["params"]}
+        return self._fused_eligible() and all(id(p) in mine for p in params)
 
     def _fused_eligible(self):
         if os.environ.get("HVK_FUSED_OPTIM", "1") == "0":  # A/B runs: the foreach path
@@ -53,9 +73,42 @@ class DecoupledSGDW(torch.optim.Optimizer):
                     return False
         return gs[0]["momentum"] != 0 and len(gs) <= 4
 
+    def _hyper_values(self):
+        gs = self.param_groups
+        lr = [float(g["lr"]) for g in gs] + [0.0] * (4 - len(gs))
+        decay = [1.0 - g["weight_decay"] * g["lr"] / g["initial_lr"] if g["weight_decay"] else 1.0
+                 for g in gs] + [1.0] * (4 - len(gs))
+        return lr, decay
+
+    def enable_device_hyper(self, device):
+        """Graph mode (trainer.capture): the fused update reads lr / decay from a device array
+        instead of kernel arguments, so a schedule still applies to captured replays."""
+        lr, decay = self._hyper_values()
+        self._hyper = torch.tensor(lr + decay, dtype=torch.float32, device=device)
+        self._hyper_ring = [(torch.empty(8, dtype=torch.float32).pin_memory(), None) for _ in range(4)]
+        self._hyper_slot = 0
+        self.device_hyper = True
+        self.hyper_used = False
+
+    def refresh_hyper(self):
+        """Copy the current lr / decay of every group into that device array, stream-ordered
+        before the next replay (a ring of pinned staging buffers: no host sync per step)."""
+        if self._hyper is None:
+            return
+        lr, decay = self._hyper_values()
+        host, ev = self._hyper_ring[self._hyper_slot]
+        if ev is not None:
+            ev.synchronize()  # that slot's previous copy (4 steps ago) has been consumed
+        host.copy_(torch.tensor(lr + decay, dtype=torch.float32))
+        self._hyper.copy_(host, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._hyper_ring[self._hyper_slot] = (host, ev)
+        self._hyper_slot = (self._hyper_slot + 1) % len(self._hyper_ring)
+
     def _fused_step(self):
-        """Clip + update of every tensor in a handful of libhvk launches (hvk_sgdw_step);
-        False (nothing done) when only some momentum buffers exist yet."""
+        """Mean + clip + update (+ EMA) of every tensor in a handful of libhvk launches
+        (hvk_sgdw_step); False (nothing done) when only some momentum buffers exist yet."""
         import ctypes
         from . import _lib
         ps, grp = [], []
@@ -76,36 +129,59 @@ class DecoupledSGDW(torch.optim.Optimizer):
         n = len(ps)
         P = ctypes.c_void_p * n
         numel = (ctypes.c_longlong * n)(*[p.numel() for p in ps])
-        arrs = (P(*[p.data_ptr() for p in ps]), P(*[p.grad.data_ptr() for p in ps]),
-                P(*[self.state[p]["momentum_buffer"].data_ptr() for p in ps]), numel,
-                (ctypes.c_int * n)(*grp))
+        arrs = [P(*[p.data_ptr() for p in ps]), P(*[p.grad.data_ptr() for p in ps]),
+                P(*[self.state[p]["momentum_buffer"].data_ptr() for p in ps])]
+        ema_arr, ema_a = None, 0.0
+        if self.pending_ema is not None:
+            emas, ema_a = self.pending_ema
+            by_id = dict(emas)
+            ema_arr = P(*[by_id[id(p)].data_ptr() for p in ps])
         gs = self.param_groups
-        lr = (ctypes.c_float * len(gs))(*[g["lr"] for g in gs])
-        decay = (ctypes.c_float * len(gs))(
-            *[1.0 - g["weight_decay"] * g["lr"] / g["initial_lr"] if g["weight_decay"] else 1.0
-              for g in gs])
+        lr_v, decay_v = self._hyper_values()
+        lr = (ctypes.c_float * 4)(*lr_v)
+        decay = (ctypes.c_float * 4)(*decay_v)
+        hyper = None
+        if self.device_hyper and self._hyper is not None:
+            hyper = _lib.ptr(self._hyper)
+            self.hyper_used = True
         lib = _lib.load()
         nb = lib.hvk_sgdw_workspace_bytes(n, ctypes.cast(numel, ctypes.c_void_p))
         if self._fused is None or self._fused.numel() * 4 < nb:
             self._fused = torch.empty(nb // 4, device=ps[0].device, dtype=torch.float32)
         clip = float(self.pending_clip) if self.pending_clip is not None else 0.0
         g0 = gs[0]
+        self._keep = (arrs, ema_arr, numel)  # ctypes tables outlive the call
         _lib.call("hvk_sgdw_step", n, *[ctypes.cast(a, ctypes.c_void_p) for a in arrs],
-                  ctypes.cast(lr, ctypes.c_void_p), ctypes.cast(decay, ctypes.c_void_p), len(gs),
-                  clip, float(g0["momentum"]), float(g0["dampening"]), int(bool(g0["nesterov"])),
-                  int(first), _lib.ptr(self._fused), nb, _lib.stream())
+                  ctypes.cast(ema_arr, ctypes.c_void_p) if ema_arr is not None else None,
+                  ctypes.cast(numel, ctypes.c_void_p), ctypes.cast((ctypes.c_int * n)(*grp), ctypes.c_void_p),
+                  ctypes.cast(lr, ctypes.c_void_p), ctypes.cast(decay, ctypes.c_void_p), len(gs), hyper,
+                  float(self.pending_grad_scale), clip, float(g0["momentum"]), float(g0["dampening"]),
+                  int(bool(g0["nesterov"])), int(first), float(ema_a), _lib.ptr(self._fused), nb,
+                  _lib.stream())
+        # the kernel wrote the weights through raw pointers: bump their version counters so
+        # version-keyed caches (ops._WeightCopies) see the update
+        torch.autograd.graph.increment_version(ps)
         return True
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        if self._fused_eligible() and self._fused_step():
+        try:
+            if self._fused_eligible() and self._fused_step():
+                return loss
+            self._foreach_step()
+        finally:
             self.pending_clip = None
-            return loss
+            self.pending_grad_scale = 1.0
+            self.pending_ema = None
+        return loss
+
+    def _foreach_step(self):
+        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if self.pending_grad_scale != 1.0 and params:
+            torch._foreach_mul_([p.grad for p in params], float(self.pending_grad_scale))
         if self.pending_clip is not None:  # unfused: clip now, as GradientClipping would
-            params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
             torch.nn.utils.clip_grad_norm_(params, self.pending_clip, foreach=True)
-            self.pending_clip = None
         for g in self.param_groups:
             ps = [p for p in g["params"] if p.grad is not None]
             if not ps:
@@ -127,7 +203,13 @@ class DecoupledSGDW(torch.optim.Optimizer):
             if wd != 0:
                 torch._foreach_mul_(ps, 1 - wd * lr / g["initial_lr"])
             torch._foreach_add_(ps, grads, alpha=-lr)
-        return loss
+        if self.pending_ema is not None:
+            emas, a = self.pending_ema
+            by_id = dict(emas)
+            ps = [p for p in params if id(p) in by_id]
+            es = [by_id[id(p)] for p in ps]
+            torch._foreach_mul_(es, a)
+            torch._foreach_add_(es, ps, alpha=1 - a)
 
 
 def build_optimizer(config, model):

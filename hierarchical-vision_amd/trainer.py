@@ -43,13 +43,24 @@ class Trainer:
         st.loss = self.model.loss(st.outputs, st.batch)
         self._run(Event.AFTER_LOSS)
         st.loss.backward()
-        self.buckets.synchronize()
+        self._grad_mean()
         self._run(Event.AFTER_BACKWARD)
         self.optimizer.step()
         self.buckets.reset()
         st.timestamp_batch += 1
         self._run(Event.BATCH_END)
         return st.loss.detach()
+
+    def _grad_mean(self, wait=True):
+        """Bucket all-reduces done -> mean gradients: handed to the optimizer as a scale when it
+        can fold it into its update (no extra pass), else divided in place."""
+        fold = self.buckets.enabled and getattr(self.optimizer, "supports_grad_scale", lambda: False)()
+        if wait:
+            self.buckets.synchronize(scale=not fold)
+        elif self.buckets.enabled and not fold:
+            self.buckets.scale_()
+        if fold:
+            self.optimizer.pending_grad_scale = 1.0 / self.buckets.world
 
     # ---------------------------------------------------------------- graph mode
     def _forward_backward(self, batch):
@@ -67,8 +78,7 @@ class Trainer:
         return st.loss.detach()
 
     def _update(self):
-        if self.buckets.enabled:
-            self.buckets.scale_()
+        self._grad_mean(wait=False)
         self._run(Event.AFTER_BACKWARD)
         self.optimizer.step()
 
@@ -95,12 +105,23 @@ class Trainer:
         self._g_bwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_bwd):
             self._g_loss = self._forward_backward(batch)
+        # lr / decay: the fused update reads them from a device array refreshed before each
+        # replay (a schedule keeps working); a foreach update has them baked in as constants
+        if hasattr(self.optimizer, "enable_device_hyper"):
+            self.optimizer.enable_device_hyper(batch[0].device)
+        self._cap_lrs = [g["lr"] for g in self.optimizer.param_groups]
         self._g_upd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_upd, pool=self._g_bwd.pool()):
             self._update()
+        self._live_hyper = getattr(self.optimizer, "hyper_used", False)
         torch.cuda.synchronize()
 
     def replay(self):
+        if self._live_hyper:
+            self.optimizer.refresh_hyper()
+        elif [g["lr"] for g in self.optimizer.param_groups] != self._cap_lrs:
+            raise RuntimeError("the captured optimizer update has its learning rates baked in "
+                               "(foreach path); a changed lr needs a new capture()")
         self._g_bwd.replay()
         if self.buckets.enabled:
             self.buckets.allreduce_now()

@@ -140,19 +140,25 @@ int hvk_weight_grad_gelu_x(const void* g, const void* h, float* dw, float* db, i
 int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* const* dst_t,
                      const int* rows, const int* cols, void* stream);
 
-/* ---- Fused optimizer step (gradient-norm clipping + DecoupledSGDW) --------------------
+/* ---- Fused optimizer step (DDP mean + gradient-norm clipping + DecoupledSGDW + EMA) ----
  * For the n f32 tensors p[k] (params), g[k] (grads), m[k] (momentum buffers) of numel[k]
- * elements in parameter group group[k] < ngroups <= 4: with coef = min(1, max_norm /
- * (||g||_2 + 1e-6)) over ALL n gradients (max_norm <= 0: coef = 1; torch clip_grad_norm_),
- * g' = coef g, m = first ? g' : momentum m + (1 - dampening) g', u = nesterov ? g' +
- * momentum m : m, p = p decay[group] - lr[group] u (composer DecoupledSGDW: decay =
- * 1 - weight_decay lr / initial_lr).  g is not modified.  workspace: f32,
- * hvk_sgdw_workspace_bytes(n, numel) bytes. */
+ * elements in parameter group group[k] < ngroups <= 4: with s = grad_scale (> 0; 1/world when
+ * g holds the SUM of the ranks' gradients, ddp.py) and coef = s min(1, max_norm /
+ * (s ||g||_2 + 1e-6)) over ALL n gradients (max_norm <= 0: coef = s; torch clip_grad_norm_ on
+ * the mean gradient), g' = coef g, m = first ? g' : momentum m + (1 - dampening) g',
+ * u = nesterov ? g' + momentum m : m, p = p decay[group] - lr[group] u (composer DecoupledSGDW:
+ * decay = 1 - weight_decay lr / initial_lr).  ema: NULL, or n pointers; then also
+ * ema[k] = a ema[k] + (1 - a) p (the updated p; a = ema_smoothing; the EMA algorithm,
+ * configs/pretrain/inat21.yaml:31-34).  hyper: NULL, or a DEVICE f32 array [8] = lr[0..3],
+ * decay[0..3] read at run time instead of lr / decay (HIP-graph replays: the host refreshes it
+ * before each replay).  g is not modified.  workspace: f32, hvk_sgdw_workspace_bytes(n, numel)
+ * bytes. */
 size_t hvk_sgdw_workspace_bytes(int n, const long long* numel);
 int hvk_sgdw_step(int n, float* const* p, const float* const* g, float* const* m,
-                  const long long* numel, const int* group, const float* lr, const float* decay,
-                  int ngroups, float max_norm, float momentum, float dampening, int nesterov,
-                  int first, float* workspace, size_t ws_bytes, void* stream);
+                  float* const* ema, const long long* numel, const int* group, const float* lr,
+                  const float* decay, int ngroups, const float* hyper, float grad_scale,
+                  float max_norm, float momentum, float dampening, int nesterov, int first,
+                  float ema_smoothing, float* workspace, size_t ws_bytes, void* stream);
 
 /* ---- W-MSA block biases (swinv2.py:218-220, 262) --------------------------------------
  * Forward: qkv_bias[3C] = (q_bias or 0, 0, 0) and eff[C] = proj_bias (or 0) + proj_w v_bias

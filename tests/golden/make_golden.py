@@ -1,7 +1,8 @@
 """Generate the golden fixtures under tests/golden/ by importing the REFERENCE
 (/root/reference, read-only) in the build container.
 
-Run:  python tests/golden/make_golden.py     (needs /root/reference; CPU only)
+Run:  python tests/golden/make_golden.py [--only index,modules,models,taxonomy,losses,swinb,prod]
+      (needs /root/reference; CPU only)
 
 The reference's third-party imports that are absent offline are replaced by
 minimal stand-ins installed into sys.modules before import:
@@ -72,7 +73,28 @@ def install_shims():
     sys.modules.update({"torchvision": tv, "torchvision.datasets": tvd})
 
 
+def sampled(name, a, n=8192):
+    """Deterministic subset of a large array (index draw from numpy default_rng seeded by
+    crc32(name), restated by tests/golden_util.py): a parity check on n entries keeps the
+    fixture small where the full tensor is hundreds of KB of incompressible floats."""
+    import zlib
+    a = np.asarray(a, np.float32).reshape(-1)
+    if a.size <= n:
+        return a
+    idx = np.random.default_rng(zlib.crc32(name.encode())).choice(a.size, n, replace=False)
+    return a[np.sort(idx)]
+
+
+def seeded(seed, shape):
+    """Inputs the tests regenerate instead of storing: standard normals, f32."""
+    return np.random.default_rng(seed).standard_normal(shape).astype(np.float32)
+
+
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="index,modules,models,taxonomy,losses,swinb,prod")
+    only = set(ap.parse_args().only.split(","))
     install_shims()
     sys.path.insert(0, REF)
     sys.path.insert(0, REPO)
@@ -84,6 +106,12 @@ def main():
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
 
+    if "swinb" in only:
+        swinb_and_prod(ref, init_params_from_rng, "swinb")
+    if "prod" in only:
+        swinb_and_prod(ref, init_params_from_rng, "prod")
+    if "index" not in only:
+        return main_rest(ref, ref_h, only)
     # ---------------------------------------------------------------- indices
     idx = {}
     for w, pws in [(7, [0, 12]), (8, [0]), (12, [0, 12]), (24, [0, 12, 6]), (6, [0])]:
@@ -114,7 +142,14 @@ def main():
         x = torch.arange(res * res, dtype=torch.float64).reshape(1, res * res, 1)
         idx[f"merge_r{res}"] = pm(x)[0].numpy().astype(np.int32)
     np.savez_compressed(os.path.join(HERE, "index_golden.npz"), **idx)
+    main_rest(ref, ref_h, only)
 
+
+def main_rest(ref, ref_h, only):
+    from oracle.hierarchy_ref import synthetic_inat_names
+    from oracle.swinv2_ref import init_params_from_rng
+    if "modules" not in only:
+        return main_models(ref, ref_h, only)
     # ---------------------------------------------------------------- modules
     mods = {}
 
@@ -171,7 +206,14 @@ def main():
     x = torch.from_numpy(rng.standard_normal((3, 5, 32)).astype(np.float32))
     run(mlp, "mlp.", x, 61)
     np.savez_compressed(os.path.join(HERE, "module_golden.npz"), **mods)
+    main_models(ref, ref_h, only)
 
+
+def main_models(ref, ref_h, only):
+    from oracle.hierarchy_ref import synthetic_inat_names
+    from oracle.swinv2_ref import init_params_from_rng
+    if "models" not in only:
+        return main_tax(ref, ref_h, only)
     # ---------------------------------------------------------------- models
     models = {}
     cfgs = {
@@ -232,7 +274,13 @@ def main():
     keys = list(ref.SwinTransformerV2(**cfgs["tiny"]).state_dict().keys())
     models["tiny.state_keys"] = np.array(keys)
     np.savez_compressed(os.path.join(HERE, "model_golden.npz"), **models)
+    main_tax(ref, ref_h, only)
 
+
+def main_tax(ref, ref_h, only):
+    from oracle.hierarchy_ref import synthetic_inat_names
+    if "taxonomy" not in only:
+        return main_loss(ref, ref_h, only)
     # ---------------------------------------------------------------- taxonomy
     tax = {}
     names = synthetic_inat_names()
@@ -268,7 +316,12 @@ def main():
         for i, v in enumerate(vecs):
             tax[f"parent.vec{i}"] = v
     np.savez_compressed(os.path.join(HERE, "taxonomy_golden.npz"), **tax)
+    main_loss(ref, ref_h, only)
 
+
+def main_loss(ref, ref_h, only):
+    if "losses" not in only:
+        return
     # ---------------------------------------------------------------- losses
     loss = {}
     sizes = (3, 13, 51, 273, 1103, 4884, 10000)
@@ -293,6 +346,70 @@ def main():
     loss["mt.smoothing"] = np.array(eps)
     np.savez_compressed(os.path.join(HERE, "loss_golden.npz"), **loss)
     print("goldens written to", HERE)
+
+
+PROD_BLOCKS = {
+    # SwinV2-T stage 0 (56x56, C 96, 3 heads, shifted) and stage 2 (14x14, C 384, 12 heads),
+    # SwinV2-B stage 0 width (C 128, 4 heads) on a 14x14 shifted map
+    "t_s0": dict(dim=96, res=56, heads=3, window=7, shift=3, batch=1, seed=100),
+    "t_s2": dict(dim=384, res=14, heads=12, window=7, shift=3, batch=2, seed=110),
+    "b_s0": dict(dim=128, res=14, heads=4, window=7, shift=3, batch=2, seed=120),
+}
+SWINB = {
+    # BASELINE configs[3] / [4] geometries (models.py registry names; swinv2.py:699-719)
+    "b224_mt": dict(img_size=224, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+                    window_size=7, num_classes=(3, 13, 51, 273, 1103, 4884, 10000),
+                    drop_path_rate=0.0),
+    "b384_w24": dict(img_size=384, embed_dim=128, depths=[2, 2, 18, 2], num_heads=[4, 8, 16, 32],
+                     window_size=24, pretrained_window_sizes=[12, 12, 12, 6], num_classes=10000,
+                     drop_path_rate=0.0),
+}
+
+
+def swinb_and_prod(ref, init_params_from_rng, which):
+    """prod_golden.npz: production-width SwinTransformerBlocks (random post-norm gammas) with
+    sampled outputs, input gradients and every parameter gradient; swinb_golden.npz: SwinV2-B
+    224 multitask and 384 w24 logits (B = 1), f32 and CPU bf16 autocast."""
+    out = {}
+    if which == "prod":
+        for name, c in PROD_BLOCKS.items():
+            blk = ref.SwinTransformerBlock(dim=c["dim"], input_resolution=(c["res"], c["res"]),
+                                           num_heads=c["heads"], window_size=c["window"],
+                                           shift_size=c["shift"])
+            shapes = {k: v.shape for k, v in blk.state_dict().items()
+                      if v.dtype.is_floating_point and not k.endswith("logit_clamp_max")
+                      and "relative_coords_table" not in k and "attn_mask" not in k}
+            blk.load_state_dict(init_params_from_rng(shapes, c["seed"]), strict=False)
+            L = c["res"] * c["res"]
+            x = torch.from_numpy(seeded(c["seed"] + 1, (c["batch"], L, c["dim"]))).requires_grad_(True)
+            y = blk(x)
+            gy = torch.from_numpy(seeded(c["seed"] + 2, tuple(y.shape)))
+            y.backward(gy)
+            pre = name + "."
+            out[pre + "y"] = sampled(pre + "y", y.detach().numpy())
+            out[pre + "gx"] = sampled(pre + "gx", x.grad.numpy())
+            for k, v in blk.named_parameters():
+                out[pre + "grad." + k] = sampled(pre + "grad." + k, v.grad.numpy())
+        np.savez_compressed(os.path.join(HERE, "prod_golden.npz"), **out)
+        return
+    for name, cfg in SWINB.items():
+        net = ref.SwinTransformerV2(**cfg).eval()
+        shapes = {k: v.shape for k, v in net.state_dict().items()
+                  if k.endswith(("weight", "bias", "logit_scale")) and "relative" not in k}
+        missing, unexpected = net.load_state_dict(init_params_from_rng(shapes, 7), strict=False)
+        assert not unexpected, unexpected
+        x = torch.from_numpy(seeded(42, (1, 3, cfg["img_size"], cfg["img_size"])))
+        with torch.no_grad():
+            y = net(x)
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                yb = net(x)
+        ys, ybs = (y, yb) if isinstance(y, list) else ([y], [yb])
+        for i, (a, b) in enumerate(zip(ys, ybs)):
+            out[f"{name}.logits{i}"] = a.numpy()
+            out[f"{name}.logits_bf16_{i}"] = b.float().numpy()
+        out[f"{name}.n_state_keys"] = np.array(len(net.state_dict()))
+        out[f"{name}.macs"] = np.array(net.flops(), np.float64)
+    np.savez_compressed(os.path.join(HERE, "swinb_golden.npz"), **out)
 
 
 class _FakeDir(str):

@@ -3,6 +3,7 @@ bucketed, hook-driven all-reduce must equal the full-batch gradient of one proce
 import os
 import socket
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -58,3 +59,79 @@ def test_bucketed_allreduce_equals_full_batch_gradient():
     for r in range(2):
         for g, p in zip(out[r], net.parameters()):
             assert torch.allclose(torch.from_numpy(g), p.grad, atol=1e-6), r
+
+
+# ---------------------------------------------------------------- the real Trainer, world 2
+MINI = dict(img_size=56, embed_dim=32, depths=(2, 2), num_heads=(1, 2), window_size=7)
+TAX_SIZES = (2, 3, 4, 5, 6, 7, 12)
+
+
+class _OracleSwin(torch.nn.Module):
+    """CPU stand-in for the SwinV2 module (whose ops are GPU-only): the oracle's f32
+    restatement (swinv2.py semantics) with its parameters as nn.Parameters, behind the
+    ComposerModel surface the Trainer drives (forward(batch), loss(outputs, batch))."""
+
+    def __init__(self, tax):
+        super().__init__()
+        from oracle import hierarchy_ref, swinv2_ref
+        self.ref, self.href = swinv2_ref, hierarchy_ref
+        shapes = swinv2_ref.state_shapes(num_classes=tax.num_leaves, **MINI)
+        init = swinv2_ref.init_params_from_rng(shapes, 3)
+        self.names = sorted(init)
+        self.ps = torch.nn.ParameterList([torch.nn.Parameter(init[n]) for n in self.names])
+        self.geom = swinv2_ref.model_geometry(**MINI)
+        self.tax = tax
+        self.lam = hierarchy_ref.hxe_level_weights("exponential", 0.1)
+
+    def forward(self, batch):
+        return self.ref.forward(dict(zip(self.names, self.ps)), batch[0], self.geom)
+
+    def loss(self, outputs, batch):
+        t = self.tax
+        return self.href.hxe_loss_torch(outputs, batch[1].numpy(), t.perm, t.node_start, t.node_end,
+                                        t.tier_base, self.lam)
+
+
+def _train(rank, world, port, out, clip, steps=2):
+    from hvamd.algorithmic import EMA, GradientClipping
+    from hvamd.hierarchy import Taxonomy
+    from hvamd.optim import DecoupledSGDW, set_weight_decay
+    from hvamd.trainer import Trainer
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    tax = Taxonomy.synthetic(TAX_SIZES)
+    model = _OracleSwin(tax)
+    opt = DecoupledSGDW(set_weight_decay(model), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    ema = EMA(half_life="4ba", update_interval="1ba")
+    trainer = Trainer(model, opt, [GradientClipping("norm", clip), ema], bucket_mb=0.05)
+    if world > 1:
+        assert len(trainer.buckets.buckets) > 2  # several all-reduces in flight in the backward
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 3, 56, 56, generator=g)
+    y = torch.from_numpy(tax.leaf_paths[[1, 5, 9, 11]])
+    per = 4 // world
+    shard = slice(rank * per, rank * per + per)
+    for _ in range(steps):
+        trainer.train_step((x[shard], y[shard]))
+    out[rank] = ([p.detach().numpy().copy() for p in model.ps],
+                 [e.numpy().copy() for e in ema.ema_params])
+    if world > 1:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("clip", [0.5, 1e4])  # clipping active / inactive (the mean must matter)
+def test_trainer_world2_equals_single_process_full_batch(clip):
+    """The real Trainer (bucketed hook-driven all-reduce with the 1/world mean handed to
+    DecoupledSGDW, GradientClipping handed over as well, EMA every batch) on two gloo ranks
+    with half the batch each: parameters and EMA weights after two steps equal one process
+    stepping on the whole batch (main.py:44-48 batch split, :104-124 DDP)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_train, args=(2, _free_port(), out, clip), nprocs=2, join=True)
+    single = {}
+    _train(0, 1, 0, single, clip)
+    for r in range(2):
+        for a, b in zip(out[r][0] + out[r][1], single[0][0] + single[0][1]):
+            assert torch.allclose(torch.from_numpy(a), torch.from_numpy(b), rtol=1e-4, atol=1e-6), r

@@ -50,3 +50,35 @@ def test_graph_replay_matches_eager():
     for (na, pa), (nb, pb) in zip(model.named_parameters(), model_b.named_parameters()):
         rel = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
         assert rel < 1e-2, (na, rel)
+
+
+def test_graph_replay_follows_lr_schedule():
+    """A learning-rate change between replays reaches the captured fused update (lr / decay
+    read from a device array refreshed before each replay) exactly as it reaches eager steps."""
+    tax, model, dev = _setup()
+    model_b = copy.deepcopy(model)
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(4, 3, 56, 56, device=dev, generator=g)
+    y = torch.tensor(tax.leaf_paths[[1, 5, 9, 11]], device=dev)
+    ta, tb = _trainer(model), _trainer(model_b)
+    for _ in range(4):
+        ta.train_step((x, y))
+    tb.capture((x, y), warmup=3)
+    tb.replay()
+    for lr in (0.2, 0.0):  # a larger step, then none: the weights must not move on lr 0
+        for t in (ta, tb):
+            for grp in t.optimizer.param_groups:
+                grp["lr"] = lr
+        ta.train_step((x, y))
+        tb.replay()
+        if lr == 0.0:
+            before = [p.detach().clone() for p in model_b.parameters()]
+            tb.replay()
+            torch.cuda.synchronize()
+            for b, p in zip(before, model_b.parameters()):
+                assert torch.equal(b, p.detach())
+            ta.train_step((x, y))
+    torch.cuda.synchronize()
+    for (na, pa), (nb, pb) in zip(model.named_parameters(), model_b.named_parameters()):
+        rel = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-2, (na, rel)

@@ -262,15 +262,20 @@ def test_prepared_weights_follow_in_place_updates():
     assert torch.equal(ops._bf16_weight(w)[0], w.bfloat16())
 
 
-def test_fused_sgdw_step_matches_foreach_path():
-    """hvk_sgdw_step (clip + DecoupledSGDW, one fused pass) against the foreach path of the same
-    optimizer on CPU copies: two steps (first-step buffer init, then the momentum update),
-    decay and no-decay groups, clipping active."""
+@pytest.mark.parametrize("gscale,ema", [(1.0, False), (0.5, True)])
+def test_fused_sgdw_step_matches_foreach_path(gscale, ema):
+    """hvk_sgdw_step (DDP mean + clip + DecoupledSGDW + EMA, one fused pass) against the
+    foreach path of the same optimizer on CPU copies: two steps (first-step buffer init, then
+    the momentum update), decay and no-decay groups, clipping active; with gscale the
+    gradients are rank sums (ddp.py) whose 1/world mean is folded into the update, with ema
+    the EMA algorithm's average (configs/pretrain/inat21.yaml:31-34) rides on the same pass."""
     from hvamd.optim import DecoupledSGDW
     torch.manual_seed(0)
     shapes = [(288, 96), (96,), (3, 1, 1), (70001,)]
     ps_gpu = [torch.nn.Parameter(torch.randn(s, device="cuda")) for s in shapes]
     ps_cpu = [torch.nn.Parameter(p.detach().cpu().clone()) for p in ps_gpu]
+    em_gpu = [p.detach().clone() + 0.1 for p in ps_gpu]
+    em_cpu = [e.cpu().clone() for e in em_gpu]
 
     def groups(ps):
         return [{"params": [ps[0], ps[2]]}, {"params": [ps[1], ps[3]], "weight_decay": 0.0}]
@@ -280,12 +285,19 @@ def test_fused_sgdw_step_matches_foreach_path():
         for pg, pc in zip(ps_gpu, ps_cpu):
             g = torch.randn(pg.shape) * 3
             pg.grad, pc.grad = g.cuda(), g.clone()
-        og.pending_clip = 2.0
+        for o, ps, es in ((og, ps_gpu, em_gpu), (oc, ps_cpu, em_cpu)):
+            o.pending_clip = 2.0
+            o.pending_grad_scale = gscale
+            if ema:
+                o.pending_ema = ([(id(p), e) for p, e in zip(ps, es)], 0.8)
+        assert og._fused_eligible()
         og.step()
-        torch.nn.utils.clip_grad_norm_(ps_cpu, 2.0)
         oc.step()
         for pg, pc in zip(ps_gpu, ps_cpu):
             assert torch.allclose(pg.detach().cpu(), pc.detach(), rtol=1e-5, atol=1e-6), step
+        for eg, ec in zip(em_gpu, em_cpu):
+            assert torch.allclose(eg.cpu(), ec, rtol=1e-5, atol=1e-6), step
+    assert og.pending_grad_scale == 1.0 and og.pending_ema is None and og.pending_clip is None
 
 
 @pytest.mark.parametrize("C", [96, 768])
