@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec/GPU SwinV2-T 224² HXE bs256; W-MSA HBM GB/s vs peak; 1→8 scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 
 
 def parse():
@@ -112,24 +113,71 @@ def measured_traffic(kernel):
         return None
 
 
-def wmsa_algorithmic_bytes(model, batch):
-    """Per-step algorithmic HBM bytes of the W-MSA kernels:
-    forward 8*T*C (bf16 qkv read 3C + out write C), backward 16*T*C."""
+def wmsa_work(model, batch):
+    """Per-step algorithmic work of the W-MSA kernels, summed over blocks with
+    each block's effective window: bytes forward 8*T*C (bf16 qkv read 3C + out write C per
+    token), backward 16*T*C; flops forward 4*T*N*C (Q K^T and P V), backward 10*T*N*C, with
+    T = batch*H*W tokens and N = w*w tokens per window."""
     from hvamd.swinv2 import SwinTransformerBlock
-    tc = 0
+    w = dict(fwd_bytes=0, bwd_bytes=0, fwd_flops=0, bwd_flops=0, windows=set())
     for m in model.modules():
         if isinstance(m, SwinTransformerBlock):
             H, W = m.input_resolution
-            tc += batch * H * W * m.dim
-    return 8 * tc, 16 * tc
+            tc = batch * H * W * m.dim
+            n = m.window_size * m.window_size
+            w["fwd_bytes"] += 8 * tc
+            w["bwd_bytes"] += 16 * tc
+            w["fwd_flops"] += 4 * tc * n
+            w["bwd_flops"] += 10 * tc * n
+            w["windows"].add(m.window_size)
+    return w
+
+
+def kernel_names(windows):
+    fwd = sorted({f"wmsa_fwd_ring_kernel<{w},HG>" if w <= 8 else f"wmsa_fwd_large_kernel<{w}>" for w in windows})
+    bwd = sorted({f"wmsa_bwd_kernel<{w}>" if w <= 8 else f"wmsa_bwd_large_kernel<{w}>" for w in windows})
+    return "+".join(fwd), "+".join(bwd)
+
+
+def roofline_block(kernel, nbytes, flops, ms_total, launches, steps, traffic):
+    """The kernel's achieved HBM rate and MFMA rate against the MI355X peaks; bound = the
+    roof its arithmetic intensity sits under (ridge = 2.5 PF / 8 TB/s = 312 flop/B)."""
+    sec = ms_total / 1000.0
+    gbs = nbytes * steps / sec / 1e9
+    tfs = flops * steps / sec / 1e12
+    ai = flops / nbytes
+    bound = "mfma" if ai > MFMA_PEAK_TFS * 1e3 / HBM_PEAK_GBS else "hbm"
+    return {"kernel": kernel, "bound": bound, "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_step": nbytes, "algorithmic_flops_per_step": flops,
+            "arith_intensity": round(ai, 1), "achieved_tflops": round(tfs, 1),
+            "mfma_frac": round(tfs / MFMA_PEAK_TFS, 4),
+            "avg_launch_us": round(1000 * ms_total / launches, 2),
+            "ms_per_step": round(ms_total / steps, 3)}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(args, seconds):
-    """The oracle's f32 CPU restatement: SwinV2-T forward + HXE + backward."""
+    """The oracle's f32 CPU restatement of the bench's model + loss (SwinV2-T 224 + HXE): train
+    steps (forward + loss + backward) at batch 32 for ~`seconds`, then ONE step at the GPU's
+    batch 256 (BASELINE.md plan).  Threads: every CPU in this process's affinity set, capped by
+    OMP_NUM_THREADS when the host sets it (the GPU box grants each GPU a 16-CPU share)."""
     from hvamd.hierarchy import Taxonomy
     from oracle import hierarchy_ref, swinv2_ref
 
-    threads = min(16, len(os.sched_getaffinity(0)))
+    affinity = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
     torch.set_num_threads(threads)
     cfg = dict(img_size=224, embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24),
                window_size=7)
@@ -139,28 +187,31 @@ def cpu_baseline(args, seconds):
         v.requires_grad_(True)
     geom = swinv2_ref.model_geometry(**cfg)
     lam = hierarchy_ref.hxe_level_weights("exponential", 0.1)
-    bs = 8
-    x = torch.randn(bs, 3, 224, 224)
-    paths = tax.leaf_paths[np.random.default_rng(0).integers(0, tax.num_leaves, bs)]
+    rng = np.random.default_rng(0)
 
-    def step():
+    def step(bs):
+        x = torch.randn(bs, 3, 224, 224)
+        paths = tax.leaf_paths[rng.integers(0, tax.num_leaves, bs)]
+        t0 = time.perf_counter()
         logits = swinv2_ref.forward(p, x, geom)
         loss = hierarchy_ref.hxe_loss_torch(logits, paths, tax.perm, tax.node_start, tax.node_end,
                                             tax.tier_base, lam)
         loss.backward()
         for v in p.values():
             v.grad = None
+        return time.perf_counter() - t0
 
-    step()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        step()
+    step(32)  # warm-up
+    n, el = 0, 0.0
+    while el < seconds and n < 50:
+        el += step(32)
         n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    return {"value": round(n * bs / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
-            "sample": f"{n} train steps x {bs} images (SwinV2-T 224 + HXE, f32, oracle/swinv2_ref.py)"}
+    t256 = step(256)
+    return {"value": round(32 * n / el, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps x 32 images (SwinV2-T 224 + HXE, f32, oracle/swinv2_ref.py); "
+                      f"one step x 256 images: {256 / t256:.3f} images/sec",
+            "bs256_images_per_sec": round(256 / t256, 3), "cpu_model": cpu_model(),
+            "affinity_cpus": affinity}
 
 
 def launch_ranks(args):
@@ -204,7 +255,7 @@ def main():
     img = model.module.patch_embed.img_size[0]
     batch = synthetic_batch(args, tax, rank, device, img)
 
-    fwd_bytes, bwd_bytes = wmsa_algorithmic_bytes(model.module, args.batch)
+    work = wmsa_work(model.module, args.batch)
     timing = not args.no_roofline
     timer, timed_steps = None, args.steps
     if args.graph:
@@ -250,6 +301,13 @@ def main():
         raise RuntimeError(f"non-finite loss {loss_val}")
     images = world * args.batch * args.steps
     value = images / elapsed
+    default_cfg = args.model == "swinv2_tiny_window7_224" and args.loss == "hxe"
+    workload = {"swinv2_tiny_window7_224": "SwinV2-T 224 w7", "swinv2_base_window7_224": "SwinV2-B 224 w7",
+                "swinv2_base_window24_384": "SwinV2-B 384 w24 (pretrained windows 12/12/12/6)"}.get(
+                    args.model, args.model)
+    workload += {"hxe": " + HXE (10000 leaves, 7 tiers)", "multitask": " + 7-tier multitask heads",
+                 "ce": " + flat 1000-class CE"}[args.loss] + " train step"
+    macs = model.module.flops()  # MACs per image, swinv2.py:847-867 accounting
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -257,9 +315,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic (randn images resident in HBM, leaves uniform over a synthetic 10k-leaf "
                 "7-tier tree); random-init weights",
-        "config": {"workload": "SwinV2-T 224 w7 + HXE (10000 leaves, 7 tiers) train step",
-                   "model": args.model, "loss": args.loss, "global_batch": world * args.batch,
-                   "per_gpu_batch": args.batch, "image_size": img,
+        "config": {"workload": workload, "model": args.model, "loss": args.loss,
+                   "global_batch": world * args.batch, "per_gpu_batch": args.batch, "image_size": img,
                    "parallelism": f"dp{world}",
                    "execution": "hip-graph replay" if args.graph else "eager"},
         "value_per_gpu": round(value / world, 2),
@@ -268,34 +325,53 @@ def main():
                   "grad_bytes_per_step": 4 * sum(b[0].numel() for b in trainer.buckets.buckets)}
                  if world > 1 else None),
         "final_loss": round(loss_val, 4),
+        # whole-step MFMA utilisation: 3 x 2 x MACs per image (forward + both backward GEMMs)
+        "step_mfma": {"flops_per_step": 6 * macs * args.batch,
+                      "achieved_tflops": round(6 * macs * args.batch * args.steps / elapsed / 1e12, 1),
+                      "peak": MFMA_PEAK_TFS,
+                      "frac": round(6 * macs * args.batch * args.steps / elapsed / 1e12 / MFMA_PEAK_TFS, 4)},
     }
     if timer:
-        fw_ms, fw_n = timer["wmsa_fwd"]
-        bw_ms, bw_n = timer["wmsa_bwd"]
+        kf, kb = kernel_names(work["windows"])
+        fw_ms, fw_n, _ = timer["wmsa_fwd"]
+        bw_ms, bw_n, _ = timer["wmsa_bwd"]
         n_launch = fw_n // timed_steps
-        fwd_gbs = fwd_bytes * timed_steps / (fw_ms / 1000) / 1e9
-        bwd_gbs = bwd_bytes * timed_steps / (bw_ms / 1000) / 1e9
-        result["roofline"] = {
-            "kernel": "wmsa_fwd_ring_kernel<7,3|4> (all %d launches per step)" % n_launch,
-            "bound": "hbm", "achieved": round(fwd_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(fwd_gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic("wmsa_fwd"),
-            "algorithmic_bytes_per_step": fwd_bytes,
-            "avg_launch_us": round(1000 * fw_ms / fw_n, 2),
-            "ms_per_step": round(fw_ms / timed_steps, 3),
-            "timing": ("dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps just "
+        traffic = measured_traffic("wmsa_fwd") if default_cfg else None
+        r = roofline_block(f"{kf} (all {n_launch} launches per step)", work["fwd_bytes"],
+                           work["fwd_flops"], fw_ms, fw_n, timed_steps, traffic)
+        r["timing"] = ("dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps just "
                        "before the graph capture (replays carry no per-kernel events)" % timed_steps
                        if args.graph else
-                       "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps")}
-        if result["roofline"]["traffic"] is not None:
-            result["roofline"]["algorithmic_bytes_per_launch"] = fwd_bytes // n_launch
-            result["roofline"]["traffic_source"] = TRAFFIC_SOURCE
-        result["roofline_bwd"] = {
-            "kernel": "wmsa_bwd_kernel<7>", "bound": "hbm", "achieved": round(bwd_gbs, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(bwd_gbs / HBM_PEAK_GBS, 4),
-            "algorithmic_bytes_per_step": bwd_bytes, "traffic": measured_traffic("wmsa_bwd"),
-            "avg_launch_us": round(1000 * bw_ms / bw_n, 2),
-            "ms_per_step": round(bw_ms / timed_steps, 3)}
-    if rank == 0 and world == 1 and args.cpu_baseline:
+                       "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps")
+        if traffic is not None:
+            r["algorithmic_bytes_per_launch"] = work["fwd_bytes"] // n_launch
+            r["traffic_source"] = TRAFFIC_SOURCE
+        result["roofline"] = r
+        result["roofline_bwd"] = roofline_block(
+            kb, work["bwd_bytes"], work["bwd_flops"], bw_ms, bw_n, timed_steps,
+            measured_traffic("wmsa_bwd") if default_cfg else None)
+        # dense contractions on libhvk's MFMA GEMMs (every Linear but the classifier head):
+        # their algorithmic flops (2 M N K per launch, summed by the library) over their
+        # dispatch-packet-timed durations
+        mf = {}
+        for kind, label in (("gemm", "linear_kernel + gemm_nt_kernel (forward, input grads)"),
+                            ("wgrad", "dw_kernel (weight grads)")):
+            ms, n, fl = timer[kind]
+            if n:
+                mf[kind] = {"kernels": label, "launches_per_step": n // timed_steps,
+                            "ms_per_step": round(ms / timed_steps, 3),
+                            "achieved_tflops": round(fl / (ms / 1000) / 1e12, 1),
+                            "frac": round(fl / (ms / 1000) / 1e12 / MFMA_PEAK_TFS, 4)}
+        tot_ms = sum(timer[k][0] for k in ("gemm", "wgrad"))
+        tot_fl = sum(timer[k][2] for k in ("gemm", "wgrad"))
+        if tot_ms > 0:
+            mf.update({"bound": "mfma", "achieved": round(tot_fl / (tot_ms / 1000) / 1e12, 1),
+                       "peak": MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                       "frac": round(tot_fl / (tot_ms / 1000) / 1e12 / MFMA_PEAK_TFS, 4),
+                       "flops_per_step": tot_fl / timed_steps,
+                       "ms_per_step": round(tot_ms / timed_steps, 3)})
+        result["mfma"] = mf
+    if rank == 0 and world == 1 and args.cpu_baseline and default_cfg:
         result["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -26,6 +26,7 @@ int hvk_abi_version(void) { return 3; }
 namespace {
 struct TimerRec {
   int kind;
+  double work;
   hipEvent_t start, stop;
 };
 std::vector<TimerRec> g_timer;  // event pool (created once, reused)
@@ -33,13 +34,14 @@ size_t g_timer_used = 0;
 bool g_timer_on = false;
 }  // namespace
 
-void hvk_timer_next(int kind, hipEvent_t* start, hipEvent_t* stop) {
+void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop) {
   if (!g_timer_on || g_timer_used >= g_timer.size()) {
     *start = *stop = nullptr;
     return;
   }
   TimerRec& r = g_timer[g_timer_used++];
   r.kind = kind;
+  r.work = work;
   *start = r.start;
   *stop = r.stop;
 }
@@ -48,7 +50,7 @@ int hvk_kernel_timer_enable(int max_launches) {
   g_timer_used = 0;
   g_timer_on = max_launches > 0;
   while (g_timer.size() < (size_t)(max_launches > 0 ? max_launches : 0)) {
-    TimerRec r{-1, nullptr, nullptr};
+    TimerRec r{-1, 0.0, nullptr, nullptr};
     if (hipEventCreate(&r.start) != hipSuccess || hipEventCreate(&r.stop) != hipSuccess)
       return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_enable: hipEventCreate failed");
     g_timer.push_back(r);
@@ -56,9 +58,9 @@ int hvk_kernel_timer_enable(int max_launches) {
   return HVK_OK;
 }
 
-int hvk_kernel_timer_read(int kind, double* total_ms, int* launches) {
+int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double* work) {
   if (!total_ms || !launches) return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_read: null pointer");
-  double t = 0.0;
+  double t = 0.0, w = 0.0;
   int n = 0;
   for (size_t i = 0; i < g_timer_used; ++i) {
     const TimerRec& r = g_timer[i];
@@ -67,11 +69,17 @@ int hvk_kernel_timer_read(int kind, double* total_ms, int* launches) {
     if (hipEventSynchronize(r.stop) != hipSuccess || hipEventElapsedTime(&ms, r.start, r.stop) != hipSuccess)
       return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_read: event query failed");
     t += ms;
+    w += r.work;
     ++n;
   }
   *total_ms = t;
   *launches = n;
+  if (work) *work = w;
   return HVK_OK;
+}
+
+int hvk_kernel_timer_read(int kind, double* total_ms, int* launches) {
+  return hvk_kernel_timer_read_work(kind, total_ms, launches, nullptr);
 }
 
 }  // extern "C"

@@ -243,12 +243,13 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   if (row_groups > need) row_groups = (need + 7) / 8 * 8;
   if (row_groups < 8) row_groups = 8;
   const dim3 grid(row_groups * ncb);
+  const double flops = 2.0 * M * N * K;
   if (bias)
-    hipLaunchKernelGGL(kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups,
-                       csum);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
+                       ncb, row_groups, csum);
   else
-    hipLaunchKernelGGL(kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N, ncb, row_groups,
-                       csum);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
+                       ncb, row_groups, csum);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }

@@ -294,8 +294,8 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   const int mtiles = (M + BM - 1) / BM;
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / T::BN));
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256), T::LDS, st, X, W, bias, Y, Y2, M, N,
-                     K, mtiles);
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
+                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }

@@ -299,12 +299,13 @@ int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, 
     attr = true;
   }
   const dim3 grid((unsigned)((p.ntiles * p.nchunk + 7) / 8 * 8));
+  const double flops = 2.0 * p.nslices * TOK * N * K;  // g^T x (the fused db adds 2 M N)
   if (with_db)
-    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, true, GX>), grid, dim3(C::THREADS), C::LDS, st, g, x, P,
-                       N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, true, GX>), grid, dim3(C::THREADS),
+                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
   else
-    hipLaunchKernelGGL((dw_kernel<FK, FN, WK, WN, false, GX>), grid, dim3(C::THREADS), C::LDS, st, g, x,
-                       P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, false, GX>), grid, dim3(C::THREADS),
+                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
   HVK_CHECK_LAUNCH("hvk_weight_grad");
   return HVK_OK;
 }

@@ -32,22 +32,27 @@ int hvk_set_error(int code, const char* fmt, ...);
 // rocprofv3 kernel trace (HIP events around a launch also count the dispatch gap).
 #define HVK_TIMER_WMSA_FWD 0
 #define HVK_TIMER_WMSA_BWD 1
+#define HVK_TIMER_GEMM 2   // forward / input-gradient GEMMs (linear_kernel, gemm_nt_kernel)
+#define HVK_TIMER_WGRAD 3  // weight-gradient GEMMs (dw_kernel; its slab reduction not included)
 #ifdef __cplusplus
 extern "C" {
 #endif
-void hvk_timer_next(int kind, hipEvent_t* start, hipEvent_t* stop);  // null pair: not timed
+// null pair: not timed; work = the launch's algorithmic flops (or bytes), summed by read
+void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop);
 #ifdef __cplusplus
 }
 #endif
-#define HVK_LAUNCH_TIMED(kind, kernel, grid, block, lds, st, ...)                       \
+#define HVK_LAUNCH_TIMED_W(kind, work, kernel, grid, block, lds, st, ...)               \
   do {                                                                                  \
     hipEvent_t e0_ = nullptr, e1_ = nullptr;                                            \
-    hvk_timer_next(kind, &e0_, &e1_);                                                   \
+    hvk_timer_next(kind, (double)(work), &e0_, &e1_);                                   \
     if (e0_)                                                                            \
       hipExtLaunchKernelGGL(kernel, grid, block, lds, st, e0_, e1_, 0, __VA_ARGS__);     \
     else                                                                                \
       hipLaunchKernelGGL(kernel, grid, block, lds, st, __VA_ARGS__);                    \
   } while (0)
+#define HVK_LAUNCH_TIMED(kind, kernel, grid, block, lds, st, ...) \
+  HVK_LAUNCH_TIMED_W(kind, 0, kernel, grid, block, lds, st, __VA_ARGS__)
 
 #define HVK_CHECK_LAUNCH(what)                                                   \
   do {                                                                           \

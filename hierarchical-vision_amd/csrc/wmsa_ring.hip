@@ -27,6 +27,9 @@
 #ifndef HVK_RING_PROBE
 #define HVK_RING_PROBE 0
 #endif
+#ifndef HVK_RING_ROWMAX_CHECK  // 0: A/B probe builds without the underflow check (not exact)
+#define HVK_RING_ROWMAX_CHECK 1
+#endif
 
 namespace {
 using namespace hvk_ring;
@@ -336,7 +339,8 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(s[ki][r]);
       pv(s);
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(tq >= 0 && !(osum[0] >= 0x1p-100f)) != 0, 0)) {
+      if (HVK_RING_ROWMAX_CHECK &&
+          __builtin_expect(__builtin_amdgcn_ballot_w64(tq >= 0 && !(osum[0] >= 0x1p-100f)) != 0, 0)) {
         // slow path (rare, wave-uniform): the tile again with the true row max over real keys,
         // one 16-key tile at a time (a second 16-register score array would spill): pass 1
         // takes the max, pass 2 exponentiates against it and accumulates P V and the row sums

@@ -14,18 +14,20 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 
-def kernel_timer_start(max_launches=8192):
-    """Time the next W-MSA launches inside libhvk (dispatch-packet events, include/hvk.h)."""
+def kernel_timer_start(max_launches=32768):
+    """Time the next W-MSA and GEMM launches inside libhvk (dispatch-packet events,
+    include/hvk.h)."""
     call("hvk_kernel_timer_enable", int(max_launches))
 
 
 def kernel_timer_stop():
-    """Stop timing; returns {"wmsa_fwd": (total_ms, launches), "wmsa_bwd": (...)}."""
+    """Stop timing; returns {"wmsa_fwd" | "wmsa_bwd" | "gemm" | "wgrad": (total_ms, launches,
+    summed algorithmic work)} (GEMM work = 2 M N K flops per launch)."""
     out = {}
-    for kind, name in ((0, "wmsa_fwd"), (1, "wmsa_bwd")):
-        t, n = ctypes.c_double(0.0), ctypes.c_int(0)
-        call("hvk_kernel_timer_read", kind, ctypes.byref(t), ctypes.byref(n))
-        out[name] = (t.value, n.value)
+    for kind, name in ((0, "wmsa_fwd"), (1, "wmsa_bwd"), (2, "gemm"), (3, "wgrad")):
+        t, n, w = ctypes.c_double(0.0), ctypes.c_int(0), ctypes.c_double(0.0)
+        call("hvk_kernel_timer_read_work", kind, ctypes.byref(t), ctypes.byref(n), ctypes.byref(w))
+        out[name] = (t.value, n.value, w.value)
     call("hvk_kernel_timer_enable", 0)
     return out
 

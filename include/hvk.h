@@ -32,12 +32,15 @@ const char* hvk_last_error_string(void);
 
 /* ---- Kernel timer (measurement only; bench.py's roofline) ---------------------------
  * enable(n > 0): time the next n launches of the timed kernels (kind 0 = W-MSA forward,
- * 1 = W-MSA backward main kernel) with start/stop events recorded by the dispatch packet
- * itself (hipExtLaunchKernelGGL): a duration is the kernel's execution, as in a rocprofv3
- * kernel trace.  enable(0) stops timing.  read() waits for the recorded launches of `kind`
- * since the last enable and returns their summed duration (ms) and count. */
+ * 1 = W-MSA backward main kernel, 2 = forward / input-gradient GEMMs, 3 = weight-gradient
+ * GEMMs) with start/stop events recorded by the dispatch packet itself
+ * (hipExtLaunchKernelGGL): a duration is the kernel's execution, as in a rocprofv3 kernel
+ * trace.  enable(0) stops timing.  read() waits for the recorded launches of `kind` since the
+ * last enable and returns their summed duration (ms) and count; read_work() also the summed
+ * algorithmic work of those launches (GEMMs: 2 M N K flops each; W-MSA: 0). */
 int hvk_kernel_timer_enable(int max_launches);
 int hvk_kernel_timer_read(int kind, double* total_ms, int* launches);
+int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double* work);
 
 /* ---- Shifted-window cosine attention core ------------------------------------------
  * Replaces swinv2.py:399-412 (roll + window_partition), 221-261 (WindowAttention core:

@@ -102,38 +102,59 @@ LARGE_SCALE_CASES = [  # ring kernels (w <= 8) incl. shifted edge windows, and t
 ]
 
 
+def _ref_grads(qkv, tab, scale, H, W, nh, win, shift, gout, amp):
+    """Oracle output and gradients in f32, or under CPU bf16 autocast (amp: the reference's own
+    AMP numerics -- bf16 q^ k^T and P V products, f32 softmax -- whose distance from f32 bounds
+    what any bf16 implementation can reach at a large logit scale)."""
+    q, t, s = (x.clone().requires_grad_(True) for x in (qkv, tab, scale))
+    with torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp):
+        y = swinv2_ref.wmsa_core_ref(q, t, s, H, W, nh, win, shift)
+    y.float().backward(gout)
+    return y.detach().float(), q.grad.float(), t.grad.float(), s.grad.float()
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
 @pytest.mark.parametrize("shared", [True, False])
 @pytest.mark.parametrize("B,H,W,nh,win,shift", LARGE_SCALE_CASES)
 def test_wmsa_scale100_anti_aligned_matches_oracle(B, H, W, nh, win, shift, shared):
     """The forward keeps the reference's softmax where the head-bound shift alone underflows:
-    finite outputs equal to the oracle's; finite gradients equal to the oracle's."""
+    finite outputs and gradients, within max(1e-2 (2e-2 for gradients), 1.5x the reference's
+    own bf16-autocast error) of the f32 oracle.  At scale 100 a bf16 rounding of q^ or k^
+    (2^-9) moves a logit by ~0.04 nats, so the reference's AMP path itself is percent-level off
+    its f32 path here; the bound follows it instead of pretending bf16 is f32."""
     import hvamd.ops as ops
     qkv, tab, scale = _anti_aligned(B, H, W, nh, win, 11, shared)
-    ref = swinv2_ref.wmsa_core_ref(qkv, tab, scale, H, W, nh, win, shift)
+    C = 32 * nh
+    gout = torch.from_numpy(np.random.default_rng(5).standard_normal((B, H * W, C)).astype(np.float32))
+    gout = gout.bfloat16().float()
+    f32 = _ref_grads(qkv, tab, scale, H, W, nh, win, shift, gout, False)
+    amp = _ref_grads(qkv, tab, scale, H, W, nh, win, shift, gout, True)
     q_gpu = qkv.cuda().bfloat16().requires_grad_(True)
     t_gpu = tab.cuda().requires_grad_(True)
     s_gpu = scale.cuda().requires_grad_(True)
     out = ops.window_attention_core(q_gpu, t_gpu, s_gpu, H, W, nh, win, shift)
-    o = out.float().cpu()
-    assert torch.isfinite(o).all()
-    rel = ((o - ref).norm() / ref.norm()).item()
-    assert rel < 1e-2, rel
-    gout = torch.from_numpy(np.random.default_rng(5).standard_normal(o.shape).astype(np.float32))
-    gout = gout.bfloat16().float()
-    q_ref, t_ref, s_ref = (x.clone().requires_grad_(True) for x in (qkv, tab, scale))
-    swinv2_ref.wmsa_core_ref(q_ref, t_ref, s_ref, H, W, nh, win, shift).backward(gout)
     out.backward(gout.cuda().bfloat16())
     torch.cuda.synchronize()
-    C = 32 * nh
+    mine = (out.detach().float().cpu(), q_gpu.grad.float().cpu(), t_gpu.grad.float().cpu(),
+            s_gpu.grad.float().cpu())
+    parts = [("out", lambda t: t, 0), ("dq", lambda t: t[..., :C], 1), ("dk", lambda t: t[..., C:2 * C], 1),
+             ("dv", lambda t: t[..., 2 * C:], 1), ("dbias", lambda t: t, 2), ("dscale", lambda t: t, 3)]
     errs = {}
-    for name, mine, r in [("dq", q_gpu.grad[..., :C], q_ref.grad[..., :C]),
-                          ("dk", q_gpu.grad[..., C:2 * C], q_ref.grad[..., C:2 * C]),
-                          ("dv", q_gpu.grad[..., 2 * C:], q_ref.grad[..., 2 * C:]),
-                          ("dbias", t_gpu.grad, t_ref.grad), ("dscale", s_gpu.grad, s_ref.grad)]:
-        mine = mine.float().cpu()
-        assert torch.isfinite(mine).all(), name
-        errs[name] = ((mine - r).norm() / r.norm().clamp_min(1e-12)).item()
-    print("ERRS", (B, H, W, nh, win, shift, shared), {k: round(v, 4) for k, v in errs.items()})
+    for name, sel, i in parts:
+        m, r, ra = sel(mine[i]), sel(f32[i]), sel(amp[i])
+        assert torch.isfinite(m).all(), name
+        if shared and name in ("dq", "dk", "dscale"):
+            # every k^ (q^) is the same unit vector up to noise: d q^ = scale sum_j dS_ij k^_j and
+            # d scale = sum dS cos cancel to the noise level (rows of dS sum to 0) -- no
+            # relative comparison is meaningful there, only finiteness
+            continue
+        base = 1e-2 if name == "out" else 2e-2
+        errs[name] = (_rel(m, r), max(base, 1.5 * _rel(ra, r)))
+    bad = {k: v for k, v in errs.items() if v[0] >= v[1]}
+    assert not bad, (bad, errs)
 
 
 def test_wmsa_rejects_unsupported_head_dim():
