@@ -72,6 +72,8 @@ SIGNATURES = {
     "hvk_ln_pool_fwd": (_i, [_p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p, _p, _p]),
     "hvk_ln_pool_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p]),
     "hvk_patchify_bf16": (_i, [_p, _p, _i, _i, _i, _i, _p]),
+    "hvk_patchify_u8_bf16": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "hvk_normalize_u8": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_multitask_ce_fwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p]),
     "hvk_multitask_ce_bwd": (_i, [_p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
     "hvk_hxe_fwd": (_i, [_p, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p]),

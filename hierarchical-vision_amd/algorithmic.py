@@ -4,10 +4,16 @@ Minimal Event / State / Algorithm surface (match(event, state) / apply(event,
 state, logger)) so the reference's `algorithms:` YAML entries drive this
 trainer the way they drive composer.Trainer (main.py:98-102).
 """
+import dataclasses
 import enum
+import logging
 import math
+import os
+import re
 
 import torch
+
+log = logging.getLogger(__name__)
 
 
 class Event(enum.Enum):
@@ -168,6 +174,92 @@ class EMA(Algorithm):
         torch._foreach_add_(self.ema_params, [p.detach() for p in params], alpha=1 - self.smoothing)
 
 
+def load_composer_model_dict(path):
+    """The model state of a composer checkpoint file: ["state"]["model"] with DDP's "module."
+    prefix stripped (algorithmic.py:141-146).  weights_only: nothing in the file executes."""
+    model_dict = torch.load(path, map_location="cpu", weights_only=True)["state"]["model"]
+    torch.nn.modules.utils.consume_prefix_in_state_dict_if_present(model_dict, "module.")
+    return model_dict
+
+
+@dataclasses.dataclass(frozen=True)
+class WandbCheckpoint:
+    """`wandb://entity/project/artifact:version?path/in/artifact` (algorithmic.py:120-147).
+    The download needs the network; a copy already in the local cache (the reference's own
+    cache layout: <cache>/wandb-artifacts/<url>/<filepath>) loads offline."""
+    source: str
+    url: str
+    filepath: str
+
+    @classmethod
+    def parse(cls, uri):
+        match = re.match(r"^wandb://([\w./-]+:[\w./-]+)\?([\w./-]+)$", uri)
+        if not match:
+            raise ValueError(f"uri '{uri}' doesn't match the pattern!")
+        return cls("wandb", *match.groups())
+
+    def local_path(self, cache):
+        return os.path.join(cache, "wandb-artifacts", self.url, self.filepath)
+
+    def load_model_dict(self, cache):
+        path = self.local_path(cache)
+        if not os.path.exists(path):
+            raise RuntimeError(f"W&B artifact {self.url} is not in the local cache ({path}) and "
+                               "downloading it needs the network")
+        return load_composer_model_dict(path)
+
+
+def parse_checkpoint(uri: str):
+    """algorithmic.py:150-157: a wandb:// or swin:// URI."""
+    from .swinv2 import Checkpoint
+    for cls in [WandbCheckpoint, Checkpoint]:
+        try:
+            return cls.parse(uri)
+        except ValueError:
+            pass
+    raise ValueError(f"Could not parse {uri}")
+
+
+class PretrainedBackbone(Algorithm):
+    """Load a pretrained backbone at INIT (algorithmic.py:35-85): the checkpoint's head keys
+    are dropped and missing head keys are not reported.  The model's `.backbone` when it has
+    one (the linear-probe wrappers), else the network itself.  Accepts wandb:// (offline from
+    the local cache) and swin:// URIs (the reference's __init__ parses wandb only)."""
+
+    def __init__(self, checkpoint, local_cache, strict):
+        self.checkpoint = parse_checkpoint(checkpoint)
+        self.local_cache = local_cache
+        self.strict = strict
+        os.makedirs(self.local_cache, exist_ok=True)
+
+    def match(self, event, state):
+        return event == Event.INIT
+
+    def apply(self, event, state, logger=None):
+        module = getattr(state.model, "module", state.model)
+        self.load_pretrained_backbone(self.checkpoint, module, self.local_cache, self.strict)
+
+    @staticmethod
+    def load_pretrained_backbone(checkpoint, model_with_backbone, local_cache, strict):
+        model_dict = checkpoint.load_model_dict(local_cache)
+        head_keys = {key for key in model_dict.keys() if "fc." in key or "head." in key}
+        for key in head_keys:
+            del model_dict[key]
+        target = getattr(model_with_backbone, "backbone", model_with_backbone)
+        own_head = {k for k in target.state_dict() if "fc." in k or "head." in k}
+        missing, unexpected = target.load_state_dict(model_dict, strict=False)
+        missing = [k for k in missing if k not in head_keys and k not in own_head
+                   and not any(n in k for n in ("relative_position_index", "relative_coords_table",
+                                                "logit_clamp_max"))]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"pretrained backbone: missing {missing}, unexpected {unexpected}")
+        if missing:
+            log.warning("Missing keys in checkpoint: %s", ", ".join(missing))
+        if unexpected:
+            log.warning("Unexpected keys in checkpoint: %s", ", ".join(unexpected))
+        return missing, unexpected
+
+
 def _not_applicable(name, why):
     class _NA(Algorithm):
         def __init__(self, *a, **k):
@@ -180,5 +272,3 @@ BlurPool = _not_applicable("BlurPool", "anti-aliased convolutions are a ResNet s
 ChannelsLast = _not_applicable("ChannelsLast", "SwinV2 activations are token-major already")
 ProgressiveResizing = _not_applicable("ProgressiveResizing",
                                       "SwinV2 has a fixed input resolution (PatchEmbed asserts it)")
-PretrainedBackbone = _not_applicable("PretrainedBackbone", "W&B artifact download needs the network; "
-                                     "load swin:// checkpoints with swinv2.Checkpoint instead")

@@ -54,14 +54,27 @@ int launch(bool scatter, const void* in, void* out, int B, int H, int W, int C, 
 
 // PatchEmbed input (swinv2.py:652-660): the 4x4/s4 Conv2d as a GEMM wants token-major
 // patches [B, (H/4)(W/4), C*16] in the conv weight's (c, py, px) order, in bf16.  One
-// thread per patch: 4C float4 row loads (neighbouring threads read neighbouring 16 B of one
-// image row) and 2C contiguous 16-B stores of its 32C-byte patch row; the bf16 rounding is
+// thread per patch: 4C row loads (neighbouring threads read neighbouring bytes of one image
+// row) and 2C contiguous 16-B stores of its 32C-byte patch row; the bf16 rounding is
 // round-to-nearest-even, as x.to(torch.bfloat16).
-template <int C>
-__global__ __launch_bounds__(256) void patchify_kernel(const float4* __restrict__ x, uint4* __restrict__ out,
-                                                       int B, int H, int W) {
+//   U8 = false: f32 images (already normalised), 16-B float4 row loads;
+//   U8 = true: the uint8 [B, C, H, W] batch of pil_image_collate (data.py:36-76) with the
+//   device-side NormalizationFn of data.py:130-136 fused in: (x - mean[c]) / std[c] in f32
+//   (correctly rounded division, as torch's sub_ + div_), one 4-B row load per (c, py).
+template <int C, bool U8>
+__global__ __launch_bounds__(256) void patchify_kernel(const void* __restrict__ xv, uint4* __restrict__ out,
+                                                       int B, int H, int W, const float* __restrict__ mean,
+                                                       const float* __restrict__ std) {
   const int GH = H >> 2, GW = W >> 2, W4 = W >> 2;
   const long long total = (long long)B * GH * GW;
+  float mu[C], sd[C];
+  if constexpr (U8) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      mu[c] = mean[c];
+      sd[c] = std[c];
+    }
+  }
   for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
        p += (long long)gridDim.x * blockDim.x) {
     const int gx = (int)(p % GW);
@@ -73,9 +86,17 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float4* __restrict_
     for (int c = 0; c < C; ++c)
 #pragma unroll
       for (int py = 0; py < 4; ++py) {
-        const float4 f = x[(((long long)b * C + c) * H + 4 * gy + py) * W4 + gx];
-        v[16 * c + 4 * py] = f.x; v[16 * c + 4 * py + 1] = f.y;
-        v[16 * c + 4 * py + 2] = f.z; v[16 * c + 4 * py + 3] = f.w;
+        const long long rowq = (((long long)b * C + c) * H + 4 * gy + py) * W4 + gx;
+        if constexpr (U8) {
+          const uint32_t u = reinterpret_cast<const uint32_t*>(xv)[rowq];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[16 * c + 4 * py + j] = __fdiv_rn((float)((u >> (8 * j)) & 0xFFu) - mu[c], sd[c]);
+        } else {
+          const float4 f = reinterpret_cast<const float4*>(xv)[rowq];
+          v[16 * c + 4 * py] = f.x; v[16 * c + 4 * py + 1] = f.y;
+          v[16 * c + 4 * py + 2] = f.z; v[16 * c + 4 * py + 3] = f.w;
+        }
       }
     uint4* o = out + p * (2 * C);
 #pragma unroll
@@ -83,24 +104,71 @@ __global__ __launch_bounds__(256) void patchify_kernel(const float4* __restrict_
   }
 }
 
+// composer NormalizationFn on its own (data.py:130-136 as the device transform, for callers
+// that want the f32 images): out = (x - mean[c]) / std[c], x uint8 [B, C, HW]; 4 pixels per
+// thread (one 4-B load, one 16-B store)
+__global__ __launch_bounds__(256) void normalize_u8_kernel(const uint32_t* __restrict__ x, float4* __restrict__ out,
+                                                           long long quads, int C, int hw4,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ std) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < quads;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)((i / hw4) % C);
+    const float m = mean[c], s = std[c];
+    const uint32_t u = x[i];
+    out[i] = make_float4(__fdiv_rn((float)(u & 0xFFu) - m, s), __fdiv_rn((float)((u >> 8) & 0xFFu) - m, s),
+                         __fdiv_rn((float)((u >> 16) & 0xFFu) - m, s), __fdiv_rn((float)(u >> 24) - m, s));
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
-int hvk_patchify_bf16(const float* x, void* out, int B, int C, int H, int W, void* stream) {
-  if (!x || !out) return hvk_set_error(HVK_EINVAL, "hvk_patchify_bf16: null pointer");
+static int patchify(const void* x, void* out, int B, int C, int H, int W, const float* mean, const float* std,
+                    void* stream, const char* who) {
+  if (!x || !out) return hvk_set_error(HVK_EINVAL, "%s: null pointer", who);
   if (B <= 0 || H <= 0 || W <= 0 || H % 4 || W % 4)
-    return hvk_set_error(HVK_EINVAL, "hvk_patchify_bf16: bad shape B=%d H=%d W=%d", B, H, W);
-  if (C != 3) return hvk_set_error(HVK_EUNSUPPORTED, "hvk_patchify_bf16: C=%d (built for 3)", C);
+    return hvk_set_error(HVK_EINVAL, "%s: bad shape B=%d H=%d W=%d", who, B, H, W);
+  if (C != 3) return hvk_set_error(HVK_EUNSUPPORTED, "%s: C=%d (built for 3)", who, C);
   const long long total = (long long)B * (H / 4) * (W / 4);
   long long grid = (total + 255) / 256;
   if (grid > 256 * 64) grid = 256 * 64;
-  hipLaunchKernelGGL(patchify_kernel<3>, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     reinterpret_cast<const float4*>(x), static_cast<uint4*>(out), B, H, W);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (mean)
+    hipLaunchKernelGGL((patchify_kernel<3, true>), dim3((unsigned)grid), dim3(256), 0, st, x,
+                       static_cast<uint4*>(out), B, H, W, mean, std);
+  else
+    hipLaunchKernelGGL((patchify_kernel<3, false>), dim3((unsigned)grid), dim3(256), 0, st, x,
+                       static_cast<uint4*>(out), B, H, W, nullptr, nullptr);
   HVK_CHECK_LAUNCH("patchify");
   return HVK_OK;
 }
 
+int hvk_patchify_bf16(const float* x, void* out, int B, int C, int H, int W, void* stream) {
+  return patchify(x, out, B, C, H, W, nullptr, nullptr, stream, "hvk_patchify_bf16");
+}
+
+int hvk_patchify_u8_bf16(const uint8_t* x, void* out, const float* mean, const float* std, int B, int C, int H,
+                         int W, void* stream) {
+  if (!mean || !std) return hvk_set_error(HVK_EINVAL, "hvk_patchify_u8_bf16: null mean / std");
+  return patchify(x, out, B, C, H, W, mean, std, stream, "hvk_patchify_u8_bf16");
+}
+
+int hvk_normalize_u8(const uint8_t* x, float* out, const float* mean, const float* std, int B, int C, int HW,
+                     void* stream) {
+  if (!x || !out || !mean || !std) return hvk_set_error(HVK_EINVAL, "hvk_normalize_u8: null pointer");
+  if (B <= 0 || C <= 0 || HW <= 0 || HW % 4)
+    return hvk_set_error(HVK_EINVAL, "hvk_normalize_u8: bad shape B=%d C=%d HW=%d", B, C, HW);
+  const long long quads = (long long)B * C * HW / 4;
+  long long grid = (quads + 255) / 256;
+  if (grid > 256 * 64) grid = 256 * 64;
+  hipLaunchKernelGGL(normalize_u8_kernel, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const uint32_t*>(x), reinterpret_cast<float4*>(out), quads, C, HW / 4,
+                     mean, std);
+  HVK_CHECK_LAUNCH("normalize_u8");
+  return HVK_OK;
+}
 
 int hvk_patch_merge_gather(const void* x, void* out, int B, int H, int W, int C, void* stream) {
   return launch(false, x, out, B, H, W, C, stream);

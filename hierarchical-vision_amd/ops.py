@@ -795,6 +795,32 @@ def patchify_bf16(x, patch):
     return out
 
 
+def patchify_u8_bf16(x, patch, mean, std):
+    """uint8 images [B, 3, H, W] -> bf16 token-major patches with the device-side
+    NormalizationFn (data.py:130-136) fused in: bf16((x - mean[c]) / std[c]) in the Conv2d
+    weight's (c, py, px) order, one kernel (hvk_patchify_u8_bf16).  mean / std: f32 [3]."""
+    B, C, H, W = x.shape
+    if x.dtype != torch.uint8:
+        raise TypeError("patchify_u8_bf16 takes uint8 images")
+    out = torch.empty((B, (H // patch) * (W // patch), C * patch * patch), device=x.device,
+                      dtype=torch.bfloat16)
+    call("hvk_patchify_u8_bf16", ptr(x.contiguous()), ptr(out), ptr(_f32(mean)), ptr(_f32(std)), B, C, H, W,
+         stream())
+    return out
+
+
+def normalize_u8(x, mean, std):
+    """composer NormalizationFn on the device: f32 (x - mean[c]) / std[c] for uint8 [B, C, H, W]
+    (hvk_normalize_u8)."""
+    B, C, H, W = x.shape
+    if x.dtype != torch.uint8:
+        raise TypeError("normalize_u8 takes uint8 images")
+    out = torch.empty((B, C, H, W), device=x.device, dtype=torch.float32)
+    call("hvk_normalize_u8", ptr(x.contiguous()), ptr(out), ptr(_f32(mean)), ptr(_f32(std)), B, C, H * W,
+         stream())
+    return out
+
+
 def patch_merge_gather(x, H, W):
     return PatchMergeGather.apply(x, H, W)
 

@@ -443,6 +443,14 @@ class PatchEmbed(nn.Module):
         self.embed_dim = embed_dim
         self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=patch_size, stride=patch_size)
         self.norm = norm_layer(embed_dim) if norm_layer is not None else None
+        self.input_norm = None  # (mean, std) f32 [C]: uint8 input normalised here (data.NormalizationFn)
+
+    def set_input_normalization(self, mean, std):
+        """Accept the raw uint8 batch of pil_image_collate and apply the device-side
+        NormalizationFn (data.py:130-136) inside the patch gather (hvk_patchify_u8_bf16)."""
+        dev = self.proj.weight.device
+        self.input_norm = (torch.as_tensor(mean, dtype=torch.float32, device=dev).reshape(-1),
+                           torch.as_tensor(std, dtype=torch.float32, device=dev).reshape(-1))
 
     def forward_stream(self, x) -> ResidualStream:
         B, C, H, W = x.shape
@@ -450,12 +458,24 @@ class PatchEmbed(nn.Module):
             f"Input image size ({H}*{W}) doesn't match model ({self.img_size[0]}*{self.img_size[1]})."
         ph, pw = self.patch_size
         gh, gw = self.patches_resolution
-        if (x.is_cuda and torch.is_autocast_enabled() and x.dtype == torch.float32 and C == 3
-                and ph == pw == 4 and not x.requires_grad):
-            patches = ops.patchify_bf16(x, 4)  # cast + patch gather in one launch
-        else:
-            xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
-            patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(B, gh * gw, C * ph * pw)
+        patches = None
+        if x.dtype == torch.uint8:
+            if self.input_norm is None:
+                raise TypeError("uint8 images need set_input_normalization(mean, std) "
+                                "(data.NormalizationFn.fuse_into)")
+            mean, std = (t.to(x.device) for t in self.input_norm)
+            if torch.is_autocast_enabled() and C == 3 and ph == pw == 4:
+                patches = ops.patchify_u8_bf16(x, 4, mean, std)  # normalise + cast + gather: one launch
+            else:
+                x = ops.normalize_u8(x, mean, std)
+        if patches is None:
+            if (x.is_cuda and torch.is_autocast_enabled() and x.dtype == torch.float32 and C == 3
+                    and ph == pw == 4 and not x.requires_grad):
+                patches = ops.patchify_bf16(x, 4)  # cast + patch gather in one launch
+            else:
+                xb = x.to(torch.bfloat16) if torch.is_autocast_enabled() else x
+                patches = xb.reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5).reshape(
+                    B, gh * gw, C * ph * pw)
         w = self.proj.weight.reshape(self.embed_dim, -1)
         if self.norm is None:
             return _as_stream(ops.linear(patches, w, self.proj.bias))

@@ -18,11 +18,19 @@ from .ddp import GradientBuckets
 
 
 class Trainer:
-    def __init__(self, model, optimizer, algorithms=(), bucket_mb=64.0, dtype=torch.bfloat16):
+    def __init__(self, model, optimizer, algorithms=(), bucket_mb=64.0, dtype=torch.bfloat16,
+                 device_transforms=None):
         self.model = model
         self.optimizer = optimizer
         self.algorithms = list(algorithms)
         self.dtype = dtype
+        # composer DataSpec device_transforms (data.py:154-164): applied to each batch on the
+        # device; a NormalizationFn the model can absorb (data.NormalizationFn.fuse_into) is
+        # folded into its patch gather once and costs no pass of its own
+        self.device_transforms = device_transforms
+        if device_transforms is not None and getattr(device_transforms, "fuse_into", None):
+            if device_transforms.fuse_into(model):
+                self.device_transforms = None
         self.state = State(model, optimizer)
         self.buckets = GradientBuckets(model, bucket_mb=bucket_mb)
         self._run(Event.INIT)
@@ -34,6 +42,8 @@ class Trainer:
 
     def train_step(self, batch):
         st = self.state
+        if self.device_transforms is not None:
+            batch = self.device_transforms(batch)
         st.batch = batch
         self.model.train()
         dev_type = batch[0].device.type
@@ -65,6 +75,8 @@ class Trainer:
     # ---------------------------------------------------------------- graph mode
     def _forward_backward(self, batch):
         st = self.state
+        if self.device_transforms is not None:
+            batch = self.device_transforms(batch)
         st.batch = batch
         self.model.train()
         if self.buckets.enabled:

@@ -261,6 +261,18 @@ int hvk_patch_merge_gather(const void* x, void* out, int B, int H, int W, int C,
  * x [B, C, H, W] -> bf16 patches [B, (H/4)(W/4), C*16] in (c, py, px) order, rounded to
  * nearest even (x.to(bfloat16) + permute + reshape in one pass).  C = 3 is built. */
 int hvk_patchify_bf16(const float* x, void* out, int B, int C, int H, int W, void* stream);
+
+/* ---- Device-side input normalisation (data.py:130-136, composer NormalizationFn) ------
+ * x: the uint8 [B, C, H, W] batch of pil_image_collate (data.py:36-76); mean / std: DEVICE f32
+ * [C] in the 0-255 scale (data.py:128-133).  hvk_patchify_u8_bf16 = NormalizationFn fused into
+ * hvk_patchify_bf16: out[b, patch, (c, py, px)] = bf16((x - mean[c]) / std[c]) (division
+ * correctly rounded, as torch's sub_ + div_ in f32, then round-to-nearest-even); C = 3,
+ * H, W multiples of 4.  hvk_normalize_u8 = the transform alone: out f32 [B, C, HW] =
+ * (x - mean[c]) / std[c] (HW a multiple of 4). */
+int hvk_patchify_u8_bf16(const uint8_t* x, void* out, const float* mean, const float* std, int B, int C, int H,
+                         int W, void* stream);
+int hvk_normalize_u8(const uint8_t* x, float* out, const float* mean, const float* std, int B, int C, int HW,
+                     void* stream);
 int hvk_patch_merge_scatter(const void* gout, void* gx, int B, int H, int W, int C,
                             void* stream);
 

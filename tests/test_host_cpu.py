@@ -221,3 +221,53 @@ def test_checkpoint_uri_and_filter():
         Checkpoint.parse("wandb://x")
     d = Checkpoint.filter({"a.relative_position_index": 1, "b.weight": 2, "c.logit_clamp_max": 3})
     assert d == {"b.weight": 2}
+
+
+def test_normalization_fn_cpu_and_channel_stats():
+    """data.channel_stats scales configs.py's 0-1 means / stds to 0-255 as build_dataspec does
+    (data.py:128-133); NormalizationFn on a CPU batch is composer's f32 (x - mean) / std."""
+    import types
+    from hvamd.data import NormalizationFn, channel_stats
+    cfg = types.SimpleNamespace(channel_mean=(0.463, 0.480, 0.376), channel_std=(0.238, 0.229, 0.247))
+    mean, std = channel_stats(cfg)
+    assert mean == [0.463 * 255, 0.480 * 255, 0.376 * 255] and std[2] == 0.247 * 255
+    x = torch.randint(0, 256, (2, 3, 8, 8), dtype=torch.uint8)
+    y, t = NormalizationFn(mean, std)((x, "t"))
+    ref = (x.float() - torch.tensor(mean).view(1, 3, 1, 1)) / torch.tensor(std).view(1, 3, 1, 1)
+    assert t == "t" and torch.equal(y, ref)
+
+
+def test_composer_and_swin_checkpoints_round_trip(tmp_path):
+    """A composer checkpoint (["state"]["model"], DDP "module." prefix; algorithmic.py:136-147)
+    and an official-Swin one (["model"] with the non-persistent buffers; swinv2.py:870-895)
+    both load weights-only into the 262-key SwinV2-T; the head is left alone (PretrainedBackbone
+    drops head keys, algorithmic.py:67-80)."""
+    from hvamd.algorithmic import PretrainedBackbone, State, WandbCheckpoint, parse_checkpoint
+    from hvamd.models import create_model
+    from hvamd.swinv2 import Checkpoint
+    torch.manual_seed(0)
+    src = create_model("swinv2_tiny_window7_224", num_classes=1000)
+    sd = src.state_dict()
+    assert len(sd) >= 262
+    wb = WandbCheckpoint.parse("wandb://team/proj/run-1:v3?ep10.pt")
+    path = wb.local_path(str(tmp_path))
+    os.makedirs(os.path.dirname(path))
+    torch.save({"state": {"model": {"module." + k: v for k, v in sd.items()}}}, path)
+    torch.save({"model": sd}, str(tmp_path / "swin.pth"))
+    for uri in ("wandb://team/proj/run-1:v3?ep10.pt", f"swin://{tmp_path}/swin.pth"):
+        dst = create_model("swinv2_tiny_window7_224", num_classes=10)
+        head = dst.head.weight.detach().clone()
+        algo = PretrainedBackbone(uri, str(tmp_path / "cache"), strict=True)
+        if isinstance(algo.checkpoint, WandbCheckpoint):
+            algo.local_cache = str(tmp_path)
+        algo.apply(None, State(dst))
+        for k, v in dst.state_dict().items():
+            if "head." in k:
+                continue
+            assert torch.equal(v, sd[k]), (uri, k)
+        assert torch.equal(dst.head.weight, head)
+    assert isinstance(parse_checkpoint(f"swin://{tmp_path}/swin.pth"), Checkpoint)
+    with pytest.raises(RuntimeError, match="network"):
+        WandbCheckpoint.parse("wandb://a/b/c:v0?x.pt").load_model_dict(str(tmp_path / "empty"))
+    with pytest.raises(ValueError):
+        parse_checkpoint("s3://bucket/x.pt")

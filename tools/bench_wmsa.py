@@ -20,17 +20,22 @@ STAGES = [  # (name, B, H, W, C, heads, window, shift, blocks per step)
 ]
 
 
-def timeit(fn, iters):
+def timeit(fn, iters, kind):
+    """Mean kernel duration (ms) from libhvk's dispatch-packet timer (execution only, as a
+    rocprofv3 kernel trace; HIP events around the launch would add the dispatch gap)."""
+    import ctypes
+    from hvamd import _lib
     for _ in range(3):
         fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    s.record()
+    _lib.call("hvk_kernel_timer_enable", 4 * iters)
     for _ in range(iters):
         fn()
-    e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+    t, n = ctypes.c_double(0.0), ctypes.c_int(0)
+    _lib.call("hvk_kernel_timer_read", kind, ctypes.byref(t), ctypes.byref(n))
+    _lib.call("hvk_kernel_timer_enable", 0)
+    return t.value / max(n.value, 1)
 
 
 def main():
@@ -71,8 +76,8 @@ def main():
             _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(dqkv), P(dqb), P(tab), P(scale), P(dtab), P(dsc),
                       P(ws), wsb, B, H, W, C, nh, win, sh, st())
 
-        tf = timeit(fwd, args.iters) if args.only != "bwd" else float("nan")
-        tb = timeit(bwd, args.iters) if args.only != "fwd" else float("nan")
+        tf = timeit(fwd, args.iters, 0) if args.only != "bwd" else float("nan")
+        tb = timeit(bwd, args.iters, 1) if args.only != "fwd" else float("nan")
         bf, bb = 8 * T * C, 16 * T * C
         tot_f += tf * nblk
         tot_b += tb * nblk
