@@ -25,7 +25,7 @@ SIGNATURES = {
     "hvk_kernel_timer_read": (_i, [_i, _p, _p]),
     "hvk_kernel_timer_read_work": (_i, [_i, _p, _p, _p]),
     "hvk_last_error_string": (ctypes.c_char_p, []),
-    "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
     "hvk_linear_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
@@ -58,7 +58,8 @@ SIGNATURES = {
     "hvk_weight_grad_gelu_x_supported": (_i, [_i, _i, _i]),
     "hvk_weight_grad_gelu_x": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
-    "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_wmsa_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i,
+                          _p]),
     "hvk_ln_residual_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _f, _p, _p, _p, _p, _p]),
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),
     "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,

@@ -40,8 +40,8 @@ struct TnCfg {
   static constexpr int CHUNKS = (REGG + REGX) / 16;          // 16-B DMA chunks per stage
   static constexpr int D = (CHUNKS + THREADS - 1) / THREADS;  // DMA instructions per lane per stage
   static constexpr int STAGE = D * THREADS * 16;
-  // the 128-wide tiles run two workgroups per CU (half the LDS each, <= 128 VGPRs)
-  static constexpr int PER_CU = TK == 128 ? 2 : 1, CAP = LDS_CAP / PER_CU;
+  // the 128 x <=192 tiles run two workgroups per CU (half the LDS each, <= 128 VGPRs)
+  static constexpr int PER_CU = (TK == 128 && TN <= 192) ? 2 : 1, CAP = LDS_CAP / PER_CU;
   static constexpr int NST = (CAP / STAGE) > 8 ? 8 : (CAP / STAGE);
   static constexpr int LDS = NST * STAGE;
   static_assert(NST >= 3, "LDS ring too shallow");
@@ -86,7 +86,7 @@ __device__ __forceinline__ void wait_stages(int r) {
 }
 
 template <int FK, int FN, int WK, int WN, bool DB, bool GX = false>
-__global__ __launch_bounds__(64 * WK * WN, 16 * FK * WK == 128 ? 2 : 1) void dw_kernel(const hvk_bf16* __restrict__ G,
+__global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN <= 192) ? 2 : 1) void dw_kernel(const hvk_bf16* __restrict__ G,
                                                            const hvk_bf16* __restrict__ X,
                                                            float* __restrict__ P, int N, int K,
                                                            int ntk, int ntiles, int nslices,
@@ -243,8 +243,9 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict
 
 // workgroup shapes: 0-3 the stage-0 Linears (whole output per workgroup), 4-7 a 192 x 192
 // or 192 x 384 tile for the rest; default 192 x 192 on 8 waves (tools/bench_dw.py: fastest
-// with the fused bias gradient on every stage 1-3 shape)
-enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C };
+// with the fused bias gradient on every stage 1-3 shape); B256 / B128: 128 x 256 and 128 x 128
+// tiles for the widths 192 does not divide (SwinV2-B: C = 128 ... 1024)
+enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C, V_B256, V_B128 };
 
 struct Plan {
   int var = -1, tk = 0, tn = 0, ntk = 0, ntiles = 0, nslices = 0, nchunk = 0;
@@ -270,13 +271,16 @@ bool plan(int M, int N, int K, Plan& p) {
     if (p.var < V_T4 || p.var > V_T8C || (p.var == V_T8W && N % 384)) p.var = V_T4;
     if (p.var == V_T8C && K % 128) p.var = V_T8A;
     p.tk = p.var == V_T8C ? 128 : 192, p.tn = p.var == V_T8W ? 384 : 192;
+  } else if (N % 128 == 0 && K % 128 == 0 && N <= 8192 && K <= 8192) {
+    p.var = N % 256 == 0 ? V_B256 : V_B128;
+    p.tk = 128, p.tn = p.var == V_B256 ? 256 : 128;
   } else {
     return false;
   }
   p.ntk = K / p.tk;
   p.ntiles = p.ntk * (N / p.tn);
   p.nslices = M / TOK;
-  int nc = (p.var == V_T8C ? 512 : 256) / p.ntiles;
+  int nc = (p.var == V_T8C || p.var == V_B128 ? 512 : 256) / p.ntiles;
   if (nc < 1) nc = 1;
   if (nc > p.nslices) nc = p.nslices;
   p.nchunk = nc;
@@ -351,6 +355,8 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
     case V_T8B: rc = launch<3, 6, 4, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_T8W: rc = launch<6, 6, 2, 4>(gb, xb, P, wd, N, K, p, st); break;
     case V_T8C: rc = launch<4, 3, 2, 4>(gb, xb, P, wd, N, K, p, st); break;
+    case V_B256: rc = launch<4, 4, 2, 4>(gb, xb, P, wd, N, K, p, st); break;
+    case V_B128: rc = launch<4, 2, 2, 4>(gb, xb, P, wd, N, K, p, st); break;
     default: rc = launch<6, 6, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
   }
   if (rc != HVK_OK) return rc;

@@ -627,10 +627,14 @@ size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
     const int n = window * window, nt = (n + 15) / 16;
     acc = (size_t)num_heads * nt * nt * 256;
   }
-  return (acc + (size_t)num_heads * 33) * sizeof(float);
+  size_t extra = 0;
+#ifdef HVK_KL_STAMP
+  extra = HVK_KL_STAMP_U64 * 2;  // diagnostic stamps after the accumulators
+#endif
+  return (acc + (size_t)num_heads * 33 + extra) * sizeof(float);
 }
 
-int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale,
+int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
                  int B, int H, int W, int C, int num_heads, int window, int shift,
                  void* stream) {
   if (!qkv || !out || !bias_table || !scale)
@@ -640,6 +644,7 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
   a.out = static_cast<hvk_bf16*>(out);
   a.bias = bias_table;
   a.scale = scale;
+  a.lse = hvk_wmsa::large_window(window) ? nullptr : lse;  // the large-window backward recomputes
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hvk_wmsa::large_window(window)) {
     int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);
@@ -653,7 +658,7 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
     const char* e = getenv("HVK_WMSA_FWD_V1");
     return e && atoi(e) > 0;
   }();
-  if (!v1) return hvk_wmsa::ring_fwd(a, B, H, W, C, num_heads, window, shift, st);
+  if (!v1 || lse) return hvk_wmsa::ring_fwd(a, B, H, W, C, num_heads, window, shift, st);
   int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);
   if (rc) return rc;
   switch (window) {
@@ -664,23 +669,32 @@ int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const floa
   }
 }
 
-int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
-                 const float* bias_table, const float* scale,
+int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float* lse, void* dqkv,
+                 float* dq_bias, const float* bias_table, const float* scale,
                  float* dbias_table, float* dscale, float* workspace, size_t workspace_bytes,
                  int B, int H, int W, int C, int num_heads, int window, int shift,
                  void* stream) {
   if (!qkv || !dout || !dqkv || !bias_table || !scale || !dbias_table || !dscale || !workspace)
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: null pointer");
+  if (lse && !out) return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: lse given without the forward's output");
   if (workspace_bytes < hvk_wmsa_bwd_workspace_bytes(num_heads, window))
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: workspace too small");
   BwdArgs a;
   a.qkv = static_cast<const hvk_bf16*>(qkv);
   a.dout = static_cast<const hvk_bf16*>(dout);
   a.dqkv = static_cast<hvk_bf16*>(dqkv);
+  a.out = static_cast<const hvk_bf16*>(out);
+  a.lse = lse;
   a.bias = bias_table;
   a.scale = scale;
+  size_t extra = 0;
+#ifdef HVK_KL_STAMP
+  extra = HVK_KL_STAMP_U64 * 2;
+  a.stamp = reinterpret_cast<unsigned long long*>(
+      workspace + hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) - extra);
+#endif
   const size_t ws_acc = hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) -
-                        (size_t)num_heads * 33;
+                        (size_t)num_heads * 33 - extra;
   a.dbias_acc = workspace;
   a.dscale_acc = workspace + ws_acc;
   a.dqb_acc = a.dscale_acc + num_heads;
@@ -690,6 +704,8 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hvk_wmsa::large_window(window))
     return hvk_wmsa::large_bwd(a, window, dbias_table, dscale, dq_bias, st);
+  // the forward's row constants given: key-on-lane kernel (wmsa_bwd.hip); else recompute them
+  if (lse) return hvk_wmsa::kl_bwd(a, window, dbias_table, dscale, dq_bias, st);
   // fill all 256 CUs: 256 / nH chunks, not rounded down to a multiple of 8 (at 12 and 24 heads
   // the rounding left 64 CUs idle), the (chunk, head) items dealt to the XCDs in runs of at
   // most 32 (one resident workgroup per CU of each XCD)

@@ -34,7 +34,7 @@
 namespace {
 using namespace hvk_ring;
 
-template <int WIN, int HG>
+template <int WIN, int HG, bool LSE>
 __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
   using K = RingCfg<WIN, HG>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -117,13 +117,14 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
   }
   if (threadIdx.x == 0) *reinterpret_cast<uint4*>(zero16) = make_uint4(0, 0, 0, 0);
   __syncthreads();
+  float Mh;  // the head bound (log2 units): L2 of a query = Mh + log2(row sum) on the fast path
   {
     float mb = -INFINITY;
     float* tb = btab + wave * K::TABF + K::TABF - K::PAD - K::R * K::R;  // mirrored real entries
     for (int i = lane; i < K::R * K::R; i += 64) mb = fmaxf(mb, tb[i]);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
-    const float Mh = a.scale[h] * HVK_LOG2E + mb;
+    Mh = a.scale[h] * HVK_LOG2E + mb;
     for (int i = lane; i < K::R * K::R; i += 64) tb[i] -= Mh;
   }
   const float sc2 = a.scale[h] * HVK_LOG2E;
@@ -178,12 +179,12 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
   issue(cb, cwh, cww);
   const uint32_t zaddr = lds_addr(zero16);
   for (int w = w0; w < w1; ++w) {
-    // this window's slab has landed: at w > w0 the NT output stores of the previous window
-    // were issued after its DMA and may still be in flight
+    // this window's slab has landed: at w > w0 the NT output stores (+ NT row-constant stores
+    // with LSE) of the previous window were issued after its DMA and may still be in flight
     if (w == w0)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::NT) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LSE ? 2 * K::NT : K::NT) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
@@ -339,6 +340,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[ki][r] = __builtin_amdgcn_exp2f(s[ki][r]);
       pv(s);
+      float lshift = 0.f;  // the slow path's row max (log2 units), on top of Mh
       if (HVK_RING_ROWMAX_CHECK &&
           __builtin_expect(__builtin_amdgcn_ballot_w64(tq >= 0 && !(osum[0] >= 0x1p-100f)) != 0, 0)) {
         // slow path (rare, wave-uniform): the tile again with the true row max over real keys,
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
         }
         m = fmaxf(m, __shfl_xor(m, 16));  // the 4 lanes (gq) holding one query's keys
         m = fmaxf(m, __shfl_xor(m, 32));
+        lshift = m;
         o[0] = o[1] = osum = hvk_f32x4{0, 0, 0, 0};
 #pragma unroll
         for (int c = 0; c < K::NC; ++c) {
@@ -402,15 +405,18 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
                                    hvk_pack2(o[0][2] * inv, o[0][3] * inv),
                                    hvk_pack2(o[1][0] * inv, o[1][1] * inv),
                                    hvk_pack2(o[1][2] * inv, o[1][3] * inv));
-        hvk_bf16* dst = a.out + (size_t)window_token_row(g, b, wh, ww, WIN, tq) * C + h * 32 + 8 * gq;
-        ring_store(dst, v);
+        const int trow = window_token_row(g, b, wh, ww, WIN, tq);
+        ring_store(a.out + (size_t)trow * C + h * 32 + 8 * gq, v);
+        if constexpr (LSE) {  // one lane per query: L2 = log2 sum_k exp2(log2e logit)
+          if (gq == 0) a.lse[(size_t)trow * g.nH + h] = Mh + lshift + __log2f(osum[0]);
+        }
       }
     }
   }
 }
 
-template <int WIN, int HG>
-int launch_ring(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
+template <int WIN, int HG, bool LSE>
+int launch_ring_(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
   using K = RingCfg<WIN, HG>;
   const int per_cu = (160 * 1024) / K::LDS;
   int rc = make_geom(B, H, W, C, nH, WIN, shift, 256 * per_cu * HG, a.g);  // capacity in groups*chunks
@@ -423,14 +429,20 @@ int launch_ring(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipSt
   a.g.n_chunks = chunks < need ? chunks : need;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_ring_kernel<WIN, HG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_ring_kernel<WIN, HG, LSE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
     attr = true;
   }
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_ring_kernel<WIN, HG>), dim3(a.g.n_chunks * ng),
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_ring_kernel<WIN, HG, LSE>), dim3(a.g.n_chunks * ng),
                    dim3(64 * HG), K::LDS, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd_ring");
   return HVK_OK;
+}
+
+template <int WIN, int HG>
+int launch_ring(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
+  return a.lse ? launch_ring_<WIN, HG, true>(a, B, H, W, C, nH, shift, st)
+               : launch_ring_<WIN, HG, false>(a, B, H, W, C, nH, shift, st);
 }
 
 template <int WIN>

@@ -351,6 +351,9 @@ def _wmsa_workspace(device, nbytes):
     return ws
 
 
+_WMSA_KL = os.environ.get("HVK_WMSA_BWD_KL", "0") == "1"  # 1: key-on-lane backward (probe)
+
+
 class WindowAttentionCore(torch.autograd.Function):
     """Shifted-window cosine attention core on un-partitioned tokens.
 
@@ -358,7 +361,10 @@ class WindowAttentionCore(torch.autograd.Function):
     without v_bias (the caller folds proj.weight @ v_bias into proj's bias).  Stands in for
     swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h).  `q_bias` is taken only to
     route its gradient: d loss / d q_bias = column sums of dq, produced by the backward
-    kernel (the qkv GEMM gets the bias detached, so no separate reduction runs)."""
+    kernel (the qkv GEMM gets the bias detached, so no separate reduction runs).  For windows
+    <= 8 the forward also keeps each query's softmax row constant (4 B per token and head) and
+    the backward takes it with the output (kept anyway as proj's saved input) instead of
+    recomputing the softmax."""
 
     @staticmethod
     def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift):
@@ -370,16 +376,23 @@ class WindowAttentionCore(torch.autograd.Function):
         bias_table = _f32(bias_table)
         scale = _f32(scale)
         out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
-        call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(bias_table), ptr(scale), B, H, W, C,
+        lse = (torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32)
+               if _WMSA_KL and window <= 8 else None)
+        call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(lse), ptr(bias_table), ptr(scale), B, H, W, C,
              num_heads, window, shift, stream())
-        ctx.save_for_backward(qkv, bias_table, scale)
+        if lse is not None:
+            ctx.save_for_backward(qkv, bias_table, scale, out, lse)
+        else:
+            ctx.save_for_backward(qkv, bias_table, scale)
         ctx.geom = (B, H, W, C, num_heads, window, shift)
         ctx.has_q_bias = q_bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, bias_table, scale = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        qkv, bias_table, scale = saved[:3]
+        out, lse = saved[3:] if len(saved) == 5 else (None, None)
         B, H, W, C, nh, win, shift = ctx.geom
         dout = _bf16(dout)
         dqkv = torch.empty_like(qkv)
@@ -389,7 +402,7 @@ class WindowAttentionCore(torch.autograd.Function):
                if ctx.has_q_bias and ctx.needs_input_grad[1] else None)
         ws_bytes = _lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
         ws = _wmsa_workspace(qkv.device, ws_bytes)
-        call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(dqkv),
+        call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(out), ptr(lse), ptr(dqkv),
              ptr(dqb) if dqb is not None else None, ptr(bias_table), ptr(scale), ptr(dtab),
              ptr(dscale), ptr(ws), ws_bytes, B, H, W, C, nh, win, shift, stream())
         return dqkv, dqb, dtab, dscale, None, None, None, None, None

@@ -53,20 +53,26 @@ int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double
  * 16*sigmoid(cpb_mlp(relative_coords_table)) (swinv2.py:233-246 before the rpi gather);
  * scale: f32 [num_heads] = exp(clamp(logit_scale, max=ln 100)) (swinv2.py:230).
  * window/shift are the clamped values of swinv2.py:328-331.  head_dim must be 32; window
- * in {4, 6, 7, 8} (one wave per (window, head)) or {12, 16, 24} (one workgroup each). */
-int hvk_wmsa_fwd(const void* qkv, void* out, const float* bias_table, const float* scale,
+ * in {4, 6, 7, 8} (one wave per (window, head)) or {12, 16, 24} (one workgroup each).
+ * lse: NULL, or f32 [B*H*W, num_heads] (windows <= 8; ignored for 12/16/24): per query and
+ * head, L2 = log2 sum_k exp2(log2e * logit), the row constant of the softmax that the
+ * key-on-lane backward consumes (P = exp2(log2e * logit - L2)). */
+int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
                  int B, int H, int W, int C, int num_heads, int window, int shift,
                  void* stream);
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
-/* dout: bf16 [B*H*W, C] (grad of `out`); dqkv: bf16 [B*H*W, 3C] (fully overwritten);
+/* dout: bf16 [B*H*W, C] (grad of `out`); out, lse: the forward's output and row constants
+ * (windows <= 8: the key-on-lane kernel, delta = rowsum(dout o out) instead of a recomputed
+ * softmax), or both NULL (every window: the softmax is recomputed from q, k);
+ * dqkv: bf16 [B*H*W, 3C] (fully overwritten);
  * dq_bias: f32 [C] (overwritten: column sums of the q part of dqkv = d loss / d q_bias,
  * replacing the qkv bias-gradient reduction) or NULL; dbias_table: f32 [num_heads,
  * (2w-1)^2] (overwritten); dscale: f32 [num_heads] (overwritten, d loss / d scale).
  * workspace: f32, hvk_wmsa_bwd_workspace_bytes bytes, ALL ZERO on entry and left all zero
  * on return (a caller keeps one zero-filled workspace: no memset per call). */
-int hvk_wmsa_bwd(const void* qkv, const void* dout, void* dqkv, float* dq_bias,
-                 const float* bias_table, const float* scale, float* dbias_table, float* dscale,
-                 float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
+int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float* lse, void* dqkv,
+                 float* dq_bias, const float* bias_table, const float* scale, float* dbias_table,
+                 float* dscale, float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
                  int num_heads, int window, int shift, void* stream);
 
 /* ---- Skinny Linear (memory-bound GEMM) ------------------------------------------------

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib.SIGNATURES), set(declared) ^ set(_lib.SIGNATURES)
     lib = _lib.load()
-    assert lib.hvk_abi_version() == 3
+    assert lib.hvk_abi_version() == 4
     # [accumulators][dscale nH][dq_bias 32 nH] floats
     assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
     assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4
@@ -40,7 +40,7 @@ def test_library_rejects_bad_arguments_without_gpu():
     """Argument validation runs on the host before any launch."""
     from hvamd import _lib
     lib = _lib.load()
-    rc = lib.hvk_wmsa_fwd(None, None, None, None, 1, 7, 7, 96, 3, 7, 0, None)
+    rc = lib.hvk_wmsa_fwd(None, None, None, None, None, 1, 7, 7, 96, 3, 7, 0, None)
     assert rc == 1 and b"null" in lib.hvk_last_error_string()
     rc = lib.hvk_patch_merge_gather(ctypes.c_void_p(16), ctypes.c_void_p(16), 1, 7, 7, 32, None)
     assert rc == 1  # odd H
