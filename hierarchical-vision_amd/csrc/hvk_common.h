@@ -246,6 +246,18 @@ __device__ __forceinline__ float hvk_xor32_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// Two 4-channel halves of a 16x16 MFMA accumulator pair (rows 4gq..4gq+3 of tile 0 = channels
+// 4gq..+3, of tile 1 = 16 + 4gq..+3; bf16-packed, lo/hi pairs) -> the 8 consecutive channels
+// this lane stores with one 16-B store, at channel offset hvk_pair_col(gq): one
+// v_permlane16_swap per dword exchanges tile 1 of the even rows (16 lanes) with tile 0 of the
+// odd rows.  Every lane of the wave must execute it (cross-lane).
+__device__ __forceinline__ uint4 hvk_pair_swap(uint2 t0, uint2 t1) {
+  const auto a = __builtin_amdgcn_permlane16_swap(t0.x, t1.x, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(t0.y, t1.y, false, false);
+  return make_uint4(a[0], b[0], a[1], b[1]);
+}
+__device__ __forceinline__ int hvk_pair_col(int gq) { return 16 * (gq & 1) + 8 * (gq >> 1); }
+
 __device__ __forceinline__ float hvk_group4_sum(float v) { return hvk_xor32_sum(hvk_xor16_sum(v)); }
 __device__ __forceinline__ float hvk_group4_max(float v) { return hvk_xor32_max(hvk_xor16_max(v)); }
 

@@ -108,8 +108,14 @@ int hvk_cast_weights(int n, const float* const* src, void* const* dst, void* con
   for (int base = 0; base < n; base += kMaxT) {
     CastBatch b;
     b.n = n - base < kMaxT ? n - base : kMaxT;
-    bool v4 = true;  // every weight of the batch with rows and cols multiples of 4
-    for (int i = 0; i < b.n; ++i) v4 = v4 && rows[base + i] % 4 == 0 && cols[base + i] % 4 == 0;
+    // the 16-B-load kernel: every weight of the batch with rows and cols multiples of 4, the f32
+    // source 16-B aligned and the bf16 copies 8-B aligned (a view into a flat buffer may not be)
+    bool v4 = true;
+    for (int i = 0; i < b.n; ++i) {
+      const int k = base + i;
+      v4 = v4 && rows[k] % 4 == 0 && cols[k] % 4 == 0 && (uintptr_t)src[k] % 16 == 0 &&
+           (uintptr_t)dst[k] % 8 == 0 && (!dst_t || (uintptr_t)dst_t[k] % 8 == 0);
+    }
     const int T = v4 ? 64 : 32;
     int tiles = 0;
     for (int i = 0; i < b.n; ++i) {

@@ -451,18 +451,20 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       }
       dot = hvk_group4_sum(dot);
       if (rnq[qi] >= 1e12f) dot = 0.f;  // ||q|| <= eps: x / eps, no projection term
-      if (q < K::N) {
-        hvk_bf16* dst = a.dqkv + (size_t)row[qi] * C3 + h * 32 + 4 * gq;
+      {
+        uint2 pk[2];
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[qi];
-            dqb[dt][r] += v[r];
+            if (q < K::N) dqb[dt][r] += v[r];
           }
-          hvk_st8(dst + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
+          pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
         }
+        const uint4 o = hvk_pair_swap(pk[0], pk[1]);  // all lanes: cross-lane
+        if (q < K::N) hvk_st16(a.dqkv + (size_t)row[qi] * C3 + h * 32 + hvk_pair_col(gq), o);
       }
     }
     asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
@@ -502,16 +504,21 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       }
       dot = hvk_group4_sum(dot);
       if (rnk[kt] >= 1e12f) dot = 0.f;
-      if (key < K::N) {
-        hvk_bf16* dst = a.dqkv + (size_t)row[kt] * C3 + h * 32 + 4 * gq;
+      {
+        uint2 pk[2], pv[2];
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rnk[kt];
-          hvk_st8(dst + C + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
-          hvk_st8(dst + 2 * C + 16 * dt,
-                  make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
+          pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+          pv[dt] = make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
+        }
+        const uint4 ok = hvk_pair_swap(pk[0], pk[1]), ov = hvk_pair_swap(pv[0], pv[1]);
+        if (key < K::N) {
+          hvk_bf16* dst = a.dqkv + (size_t)row[kt] * C3 + h * 32 + hvk_pair_col(gq);
+          hvk_st16(dst + C, ok);
+          hvk_st16(dst + 2 * C, ov);
         }
       }
     }

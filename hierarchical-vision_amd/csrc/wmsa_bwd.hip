@@ -30,6 +30,12 @@
 #ifndef HVK_KL_MINB
 #define HVK_KL_MINB 2
 #endif
+#ifndef HVK_KL_PROBE
+#define HVK_KL_PROBE 0
+#endif
+#ifndef HVK_KL_SPLIT
+#define HVK_KL_SPLIT 0
+#endif
 #ifndef HVK_KL_SB
 #define HVK_KL_SB 1
 #endif
@@ -42,6 +48,12 @@ struct BCfg {
   using RC = RingCfg<WIN, 1>;
   static constexpr int PW = RC::PW, NT = RC::NT, NC = RC::NC, R = RC::R, TR = RC::TR;
   static constexpr int HALF = (NT + 1) / 2;      // key / query tiles per wave (wave 1: NT - HALF)
+  // waves per workgroup: two (tiles [0, HALF) and [HALF, NT)) or, HVK_KL_SPLIT, one per tile
+  static constexpr int NW = HVK_KL_SPLIT ? NT : (NT > 1 ? 2 : 1);
+  template <int W>
+  static constexpr int t0() { return HVK_KL_SPLIT ? W : (W == 0 ? 0 : HALF); }
+  template <int W>
+  static constexpr int ntl() { return HVK_KL_SPLIT ? 1 : (W == 0 ? HALF : NT - HALF); }
   static constexpr int ROWS = 32 * NC;           // token slots of the [ROWS][32] bf16 images
   static constexpr int IMG = ROWS * 64;          // bytes of one such image
   static constexpr int DSI = ROWS * ROWS * 2;    // dS image: [ROWS keys][ROWS queries] bf16
@@ -60,7 +72,6 @@ struct BCfg {
   static_assert(TAB * 4 <= SHARED, "the workgroup reduction reuses the images");
 };
 
-constexpr int kWaves = 2;
 
 // dS image [ROWS keys][ROWS q] bf16, 8-B units XOR-swizzled by row (wmsa.hip pimg_off): the
 // 8-B writes of a key tile and the transposed reads of dQ are bank-conflict free
@@ -274,17 +285,22 @@ __device__ __forceinline__ void key_tiles(const BwdArgs& a, const Lane& L, int h
     }
     dot = hvk_group4_sum(dot);
     if (rnk[j] >= 1e12f) dot = 0.f;  // ||k|| <= eps: x / eps, no projection term
-    if (kvalid) {
-      hvk_bf16* dst = a.dqkv + (size_t)row[j] * C3 + h * 32 + 4 * gq;
+    {
       const float f = rnk[j] * (1.f / HVK_LOG2E);  // scale dS q^ = dS (scale log2e q^) / log2e
+      uint2 pk[2], pv[2];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * f;
-        hvk_st8(dst + C + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
-        hvk_st8(dst + 2 * C + 16 * dt,
-                make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
+        pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+        pv[dt] = make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
+      }
+      const uint4 ok = hvk_pair_swap(pk[0], pk[1]), ov = hvk_pair_swap(pv[0], pv[1]);
+      if (kvalid) {
+        hvk_bf16* dst = a.dqkv + (size_t)row[j] * C3 + h * 32 + hvk_pair_col(gq);
+        hvk_st16(dst + C, ok);
+        hvk_st16(dst + 2 * C, ov);
       }
     }
   }
@@ -333,19 +349,22 @@ __device__ __forceinline__ void query_tiles(const BwdArgs& a, const Lane& L, int
     }
     dot = hvk_group4_sum(dot);
     if (rnq[j] >= 1e12f) dot = 0.f;
-    if (pos_valid<WIN>(pq)) {
-      hvk_bf16* dst = a.dqkv + (size_t)row[j] * C3 + h * 32 + 4 * gq;
+    {
+      const bool ok = pos_valid<WIN>(pq);
       const float f = L.scale * rnq[j];
+      uint2 pk[2];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v[r] = (dq[dt][r] - qh[dt][r] * dot) * f;
-          dqb[dt][r] += v[r];
+          if (ok) dqb[dt][r] += v[r];
         }
-        hvk_st8(dst + 16 * dt, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
+        pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
       }
+      const uint4 o = hvk_pair_swap(pk[0], pk[1]);
+      if (ok) hvk_st16(a.dqkv + (size_t)row[j] * C3 + h * 32 + hvk_pair_col(gq), o);
     }
   }
 }
@@ -355,8 +374,8 @@ template <int WIN, int W>
 __device__ __forceinline__ void pair_wave(const BwdArgs& a, Lane L, int h, int w0, int w1, char* smem,
                                           const float* tl) {
   using K = BCfg<WIN>;
-  constexpr int T0 = W == 0 ? 0 : K::HALF;
-  constexpr int NTL = W == 0 ? K::HALF : K::NT - K::HALF;
+  constexpr int T0 = K::template t0<W>();
+  constexpr int NTL = K::template ntl<W>();
   constexpr int NA = NTL > 0 ? NTL : 1;
   const WmsaGeom& g = a.g;
   char* qimg = smem;
@@ -384,6 +403,25 @@ __device__ __forceinline__ void pair_wave(const BwdArgs& a, Lane L, int h, int w
 #endif
   Raw<NTL> raw;
   load_raw<WIN, T0, NTL>(a, L, h, w0, raw);
+#if HVK_KL_PROBE == 1
+  // memory-only probe (not the product): the same loads and 16-B stores, no math, no barriers
+  for (int w = w0; w < w1; ++w) {
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) {
+      const int p = 16 * (T0 + j) + L.li;
+      uint4 x = raw.q[j];
+      x.x ^= raw.d[j].x ^ raw.o[j].x ^ __float_as_uint(raw.l2[j]);
+      if (pos_valid<WIN>(p)) {
+        hvk_bf16* dst = a.dqkv + (size_t)raw.row[j] * 3 * g.C + h * 32 + 8 * L.gq;
+        hvk_st16(dst, x);
+        hvk_st16(dst + g.C, raw.k[j]);
+        hvk_st16(dst + 2 * g.C, raw.v[j]);
+      }
+    }
+    load_raw<WIN, T0, NTL>(a, L, h, w + 1 < w1 ? w + 1 : w, raw);
+  }
+  return;
+#endif
   for (int w = w0; w < w1; ++w) {
     const int rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
     L.edge_r = g.shift && wh == g.nWh - 1;
@@ -428,7 +466,7 @@ __device__ __forceinline__ void pair_wave(const BwdArgs& a, Lane L, int h, int w
           make_float4(dbias[qi][j][0], dbias[qi][j][1], dbias[qi][j][2], dbias[qi][j][3]);
   __syncthreads();
   float* dst = a.dbias_acc + (size_t)h * K::TAB;
-  for (int e = threadIdx.x; e < K::TAB; e += 64 * kWaves) atomicAdd(dst + e, red[e]);
+  for (int e = threadIdx.x; e < K::TAB; e += 64 * K::NW) atomicAdd(dst + e, red[e]);
   dsc = hvk_wave_sum(dsc);
   if (threadIdx.x == 64 * W) atomicAdd(a.dscale_acc + h, dsc);
 #pragma unroll
@@ -441,7 +479,7 @@ __device__ __forceinline__ void pair_wave(const BwdArgs& a, Lane L, int h, int w
 }
 
 template <int WIN>
-__global__ __launch_bounds__(64 * kWaves, HVK_KL_MINB) void wmsa_bwd_kl_kernel(BwdArgs a) {
+__global__ __launch_bounds__(HVK_KL_SPLIT ? 256 : 128, HVK_KL_MINB) void wmsa_bwd_kl_kernel(BwdArgs a) {
   using K = BCfg<WIN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WmsaGeom& g = a.g;
@@ -459,13 +497,13 @@ __global__ __launch_bounds__(64 * kWaves, HVK_KL_MINB) void wmsa_bwd_kl_kernel(B
   L.scale = a.scale[h];
   L.sc2 = L.scale * HVK_LOG2E;
   float* tab = reinterpret_cast<float*>(smem + K::SHARED);
-  for (int e = threadIdx.x; e < K::TABF; e += 64 * kWaves) {
+  for (int e = threadIdx.x; e < K::TABF; e += 64 * K::NW) {
     const int j = e - K::PAD;
     tab[e] = (j >= 0 && j < K::R * K::R) ? a.bias[(size_t)h * K::R * K::R + j] * HVK_LOG2E : 0.f;
   }
   {  // zero the images once: rows of padding tokens are never written again
     uint4* z = reinterpret_cast<uint4*>(smem);
-    for (int e = threadIdx.x; e < K::SHARED / 16; e += 64 * kWaves) z[e] = make_uint4(0, 0, 0, 0);
+    for (int e = threadIdx.x; e < K::SHARED / 16; e += 64 * K::NW) z[e] = make_uint4(0, 0, 0, 0);
   }
   // lane-constant table pointer: entry TR (qi - kt + NT - 1) + r sits at tl + that offset
   int lq, lk;
@@ -479,8 +517,12 @@ __global__ __launch_bounds__(64 * kWaves, HVK_KL_MINB) void wmsa_bwd_kl_kernel(B
   const float* tl = tab + K::PAD + lq - lk - K::TR * (K::NT - 1);
   if (wave == 0)
     pair_wave<WIN, 0>(a, L, h, w0, w1, smem, tl);
-  else
-    pair_wave<WIN, 1>(a, L, h, w0, w1, smem, tl);
+  else if (K::NW > 1 && wave == 1)
+    pair_wave<WIN, (K::NW > 1 ? 1 : 0)>(a, L, h, w0, w1, smem, tl);
+  else if (K::NW > 2 && wave == 2)
+    pair_wave<WIN, (K::NW > 2 ? 2 : 0)>(a, L, h, w0, w1, smem, tl);
+  else if (K::NW > 3)
+    pair_wave<WIN, (K::NW > 3 ? 3 : 0)>(a, L, h, w0, w1, smem, tl);
 }
 
 // Bin the accumulator-order partial sums ([qi][kt][lane][r]: query 16qi + 4(lane>>4) + r, key
@@ -543,7 +585,7 @@ int launch_kl(BwdArgs& a, float* dtab, float* dscale, float* dqb, hipStream_t st
   if (!per_cu) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(&wmsa_bwd_kl_kernel<WIN>),
-                                                     64 * kWaves, K::LDS) != hipSuccess || nb < 1)
+                                                     64 * K::NW, K::LDS) != hipSuccess || nb < 1)
       nb = 1;
     per_cu = nb;
   }
@@ -553,7 +595,7 @@ int launch_kl(BwdArgs& a, float* dtab, float* dscale, float* dqb, hipStream_t st
   a.g.xcd_runs = 1;
   const int items = a.g.n_chunks * a.g.nH;
   HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kl_kernel<WIN>, dim3(8 * ((items + 7) / 8)),
-                   dim3(64 * kWaves), K::LDS, st, a);
+                   dim3(64 * K::NW), K::LDS, st, a);
   HVK_CHECK_LAUNCH("wmsa_bwd_kl");
   hipLaunchKernelGGL(wmsa_bwd_kl_finalize<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dtab, dscale, dqb);
   HVK_CHECK_LAUNCH("wmsa_bwd_kl_finalize");

@@ -19,6 +19,18 @@
 // bank-conflict free (checked with the LDS bank model of MI355X_MICROARCH.md).
 #include "wmsa_common.h"
 
+// experiment builds (not the product): 1 no CPB-gradient LDS atomics, 2 also no CPB gathers
+#ifndef HVK_LARGE_PROBE
+#define HVK_LARGE_PROBE 0
+#endif
+#ifndef HVK_LARGE_BINS
+#define HVK_LARGE_BINS 1
+#endif
+#ifndef HVK_LARGE_QSTRIDE
+#define HVK_LARGE_QSTRIDE 1
+#endif
+#define LTAB(i) (HVK_LARGE_PROBE >= 2 ? 0.f : tab[i])
+
 namespace hvk_wmsa {
 namespace {
 
@@ -35,6 +47,13 @@ struct LCfg {
   static constexpr int QB = (NT % (2 * WAVES) == 0) ? 2 : 1;  // query tiles per forward pass
   static constexpr int IMG = ROWS * 64;        // bytes per image
   static_assert(NT % WAVES == 0 || QB == 1, "tile split");
+  static_assert(N == 16 * NT, "strided query tiles cover the window exactly");
+  // backward: BWAVES waves, each with a private copy of the CPB-gradient bins (plain LDS
+  // read-add-write, no float atomics) when HVK_LARGE_BINS; 8 waves at w24 so that the 8
+  // copies fit beside the two images
+  static constexpr int BWAVES = HVK_LARGE_BINS ? 8 : WAVES;
+  static constexpr int BTHREADS = 64 * BWAVES;
+  static constexpr int RRP = (RR + 3) / 4 * 4;  // bins per copy (16-B aligned)
 };
 
 // X^T fragment (A operand) of the 32-row chunk c, head-dim half dt, from an image of X
@@ -152,7 +171,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = s[t][r] + tab[qi[j].b - ki[t][r].b];
+            float v = s[t][r] + LTAB(qi[j].b - ki[t][r].b);
             v += mask_of(edge_r, edge_c, ki[t][r], qi[j], mask2);
             if (kpad[t][r]) v = -INFINITY;
             s[t][r] = v;
@@ -232,11 +251,12 @@ __device__ __forceinline__ void normalize_bwd_store(const hvk_bf16* x, float rn,
 template <int WIN>
 constexpr size_t bwd_large_lds() {
   using K = LCfg<WIN>;
-  return 2 * (size_t)K::IMG + 2 * (size_t)K::RR * 4 + 2 * (size_t)K::ROWS * 4;
+  const size_t bins = HVK_LARGE_BINS ? (size_t)K::BWAVES * K::RRP : (size_t)K::RR;
+  return 2 * (size_t)K::IMG + (size_t)K::RRP * 4 + bins * 4 + 2 * (size_t)K::ROWS * 4;
 }
 
 template <int WIN>
-__global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(BwdArgs a) {
+__global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(BwdArgs a) {
   using K = LCfg<WIN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WmsaGeom& g = a.g;
@@ -246,8 +266,9 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   char* img0 = smem;
   char* img1 = smem + K::IMG;
   float* tab = reinterpret_cast<float*>(smem + 2 * K::IMG);
-  float* dtab = tab + K::RR;
-  float* lse_s = dtab + K::RR;   // [ROWS] row log2-sum-exp2 (+inf for padding rows)
+  float* dtab = tab + K::RRP;    // [BWAVES][RRP] private bins (HVK_LARGE_BINS) or [RR] shared
+  constexpr int NBIN = HVK_LARGE_BINS ? K::BWAVES * K::RRP : K::RR;
+  float* lse_s = dtab + NBIN;    // [ROWS] row log2-sum-exp2 (+inf for padding rows)
   float* dlt_s = lse_s + K::ROWS;  // [ROWS] delta = rowsum(P * dP)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   const int C = g.C, C3 = 3 * C;
@@ -260,16 +281,14 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
 
   const float* bsrc = a.bias + (size_t)h * K::RR;
-  for (int e = threadIdx.x; e < K::RR; e += K::THREADS) {
-    tab[e] = bsrc[e] * HVK_LOG2E;
-    dtab[e] = 0.f;
-  }
-  for (int e = threadIdx.x; e < K::ROWS; e += K::THREADS) {
+  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) tab[e] = bsrc[e] * HVK_LOG2E;
+  for (int e = threadIdx.x; e < NBIN; e += K::BTHREADS) dtab[e] = 0.f;
+  for (int e = threadIdx.x; e < K::ROWS; e += K::BTHREADS) {
     lse_s[e] = INFINITY;
     dlt_s[e] = 0.f;
   }
   // phase-1 images: k^ and v, natural head_dim order
-  for (int t = wave; t < 2 * K::NC; t += K::WAVES) {
+  for (int t = wave; t < 2 * K::NC; t += K::BWAVES) {
     const int pos = 16 * t + li;
     uint4 kv = make_uint4(0, 0, 0, 0), vv = kv;
     if (pos < K::N) {
@@ -287,8 +306,11 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   // ---------------- phase 1: query tiles (query on the lane)
   float dscale = 0.f;
   float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  for (int qt = wave; qt < K::NT; qt += K::WAVES) {
-    const int pos = 16 * qt + li, posc = pos < K::N ? pos : K::N - 1;
+  for (int qt = wave; qt < K::NT; qt += K::BWAVES) {
+    // query tile qt = positions qt + NT*li (N = 16 NT for w 12/16/24): the 16 queries of a tile
+    // lie >= one window row apart, so the CPB-gradient atomics of one instruction (query li,
+    // key 4g + r) never share an LDS address (consecutive queries put 4 lanes on each)
+    const int pos = HVK_LARGE_QSTRIDE ? qt + K::NT * li : 16 * qt + li, posc = pos < K::N ? pos : K::N - 1;
     const bool qvalid = pos < K::N;
     const int qrow = window_token_row(g, b, wh, ww, WIN, posc);
     const hvk_bf16* qp = a.qkv + (size_t)qrow * C3 + h * 32;
@@ -312,7 +334,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
         for (int r = 0; r < 4; ++r) {
           const int key = 16 * kt + 4 * gq + r;
           const PosInfo<WIN> ki = key_info<WIN>(key < K::N ? key : K::N - 1, lim);
-          float x = s[r] + tab[qi.b - ki.b];
+          float x = s[r] + LTAB(qi.b - ki.b);
           x += mask_of(edge_r, edge_c, ki, qi, mask2);
           v[t][r] = key < K::N ? x : -INFINITY;
           dp[t][r] = d[r];
@@ -364,13 +386,26 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
           const bool kvalid = key < K::N;
           const PosInfo<WIN> ki = key_info<WIN>(kvalid ? key : K::N - 1, lim);
           const int idx = qi.b - ki.b;
-          float x = s[r] + tab[idx];
+          float x = s[r] + LTAB(idx);
           x += mask_of(edge_r, edge_c, ki, qi, mask2);
           const float p = kvalid ? __builtin_amdgcn_exp2f(x - lse) : 0.f;
           const float dsv = p * (d[r] - delta);
           ds[t][r] = dsv;
           if (kvalid && qvalid) {
-            atomicAdd(&dtab[idx], dsv);  // LDS float atomic (ds_add_f32)
+            if (HVK_LARGE_PROBE >= 1) {
+            } else if (HVK_LARGE_BINS) {
+              // this wave's own bins; the 64 lanes of one read-add-write never share a bin
+              // (strided query tiles), and a wave's LDS operations complete in order.  The
+              // compiler fences keep each read-add-write whole: without them hipcc merges the
+              // reads of a lane's adjacent bins (r, r + 1) ahead of the writes, which is
+              // exact per lane but loses the updates another lane makes in between
+              float* pb = dtab + wave * K::RRP + idx;
+              asm volatile("" ::: "memory");
+              *pb += dsv;
+              asm volatile("" ::: "memory");
+            } else {
+              atomicAdd(&dtab[idx], dsv);  // LDS float atomic (ds_add_f32)
+            }
             dscale += dsv * s[r];        // s = sc2 * cos: divided out at the end
           }
         }
@@ -388,7 +423,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   __syncthreads();
 
   // phase-2 images: q^ * scale * log2e (exactly the forward's operand) and dO
-  for (int t = wave; t < 2 * K::NC; t += K::WAVES) {
+  for (int t = wave; t < 2 * K::NC; t += K::BWAVES) {
     const int pos = 16 * t + li;
     uint4 qv = make_uint4(0, 0, 0, 0), dv = qv;
     if (pos < K::N) {
@@ -404,7 +439,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   __syncthreads();
 
   // ---------------- phase 2: key tiles (key on the lane)
-  for (int kt = wave; kt < K::NT; kt += K::WAVES) {
+  for (int kt = wave; kt < K::NT; kt += K::BWAVES) {
     const int pos = 16 * kt + li, posc = pos < K::N ? pos : K::N - 1;
     const bool kvalid = pos < K::N;
     const int krow = window_token_row(g, b, wh, ww, WIN, posc);
@@ -430,7 +465,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
         for (int r = 0; r < 4; ++r) {
           const int q = 16 * qt + 4 * gq + r;
           const PosInfo<WIN> qi = query_info<WIN>(q < K::N ? q : K::N - 1, lim);
-          float x = s[r] + tab[qi.b - ki.b];
+          float x = s[r] + LTAB(qi.b - ki.b);
           x += mask_of(edge_r, edge_c, ki, qi, mask2);
           p[t][r] = __builtin_amdgcn_exp2f(x - lr[r]);  // padding query: lse = +inf -> 0
           ds[t][r] = p[t][r] * (d[r] - dr[r]);
@@ -459,7 +494,12 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_bwd_large_kernel(B
   __syncthreads();
 
   float* gbias = a.dbias_acc + (size_t)h * K::RR;
-  for (int e = threadIdx.x; e < K::RR; e += K::THREADS) atomicAdd(gbias + e, dtab[e]);
+  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < (HVK_LARGE_BINS ? K::BWAVES : 1); ++c) v += dtab[c * K::RRP + e];
+    atomicAdd(gbias + e, v);
+  }
   dscale = hvk_wave_sum(dscale);
   if (lane == 0) atomicAdd(a.dscale_acc + h, dscale / sc2);
 #pragma unroll
@@ -513,7 +553,7 @@ int launch_bwd_large(const BwdArgs& a, float* dtab, float* dscale, float* dqb, h
     attr = true;
   }
   const int padded = (a.g.n_windows + 7) / 8 * 8;
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_large_kernel<WIN>, dim3(padded * a.g.nH), dim3(K::THREADS), lds, st, a);
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_large_kernel<WIN>, dim3(padded * a.g.nH), dim3(K::BTHREADS), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_bwd_large");
   hipLaunchKernelGGL(wmsa_finalize_large_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dtab, dscale, dqb);
   HVK_CHECK_LAUNCH("wmsa_finalize_large");

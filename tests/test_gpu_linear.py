@@ -242,6 +242,34 @@ def test_cast_weights_bit_exact_and_transposed(shapes):
         assert torch.equal(t, w.to(torch.bfloat16).t())
 
 
+def test_cast_weights_misaligned_views():
+    """Weights that are views at 4-B (not 16-B) offsets into a flat buffer, with shapes that
+    would otherwise take the 16-B-load kernel: the host falls back to the unaligned kernel."""
+    import ctypes
+    from hvamd import _lib
+    shapes = [(96, 96), (288, 96), (4, 4)]
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    flat = torch.randn(1 + sum(r * c for r, c in shapes), device="cuda", generator=gen)
+    ws, off = [], 1  # one float in: every view 4 B past a 16-B boundary
+    for r, c in shapes:
+        ws.append(flat[off:off + r * c].view(r, c))
+        off += r * c
+    assert ws[0].data_ptr() % 16 == 4
+    dst = [torch.empty(s, device="cuda", dtype=torch.bfloat16) for s in shapes]
+    dtt = [torch.empty(s[::-1], device="cuda", dtype=torch.bfloat16) for s in shapes]
+    n = len(shapes)
+    arr = ctypes.c_void_p * n
+    a = [arr(*[t.data_ptr() for t in ts]) for ts in (ws, dst, dtt)]
+    rows = (ctypes.c_int * n)(*[s[0] for s in shapes])
+    cols = (ctypes.c_int * n)(*[s[1] for s in shapes])
+    _lib.call("hvk_cast_weights", n, *[ctypes.cast(x, ctypes.c_void_p) for x in a],
+              ctypes.cast(rows, ctypes.c_void_p), ctypes.cast(cols, ctypes.c_void_p), _lib.stream())
+    torch.cuda.synchronize()
+    for w, d, t in zip(ws, dst, dtt):
+        assert torch.equal(d, w.to(torch.bfloat16))
+        assert torch.equal(t, w.to(torch.bfloat16).t())
+
+
 def test_prepared_weights_follow_in_place_updates():
     """The step's bf16 copies are used while the master is unchanged and bypassed after an
     in-place (optimizer-style) update until the next prepare."""

@@ -18,6 +18,13 @@ STAGES = [  # (name, B, H, W, C, heads, window, shift, blocks per step)
     ("stage2-s3", 256, 14, 14, 384, 12, 7, 3, 6),
     ("stage3", 256, 7, 7, 768, 24, 7, 0, 2),
 ]
+# SwinV2-B 384, windows 24/24/24/12 (pretrained 12/12/12/6), bs256: BASELINE config 5
+STAGES_B384 = [
+    ("b384-s0-s12", 256, 96, 96, 128, 4, 24, 12, 2),
+    ("b384-s1-s12", 256, 48, 48, 256, 8, 24, 12, 2),
+    ("b384-s2", 256, 24, 24, 512, 16, 24, 0, 18),
+    ("b384-s3", 256, 12, 12, 1024, 32, 12, 0, 2),
+]
 
 
 def timeit(fn, iters, kind):
@@ -66,6 +73,7 @@ def main():
     ap.add_argument("--kl", type=int, default=1, help="1: forward keeps row constants, key-on-lane backward")
     ap.add_argument("--stamps", action="store_true",
                     help="diagnostic build (-DHVK_KL_STAMP): per-phase cycles of the key-on-lane backward")
+    ap.add_argument("--b384", action="store_true", help="SwinV2-B 384 w24 stage shapes (config 5)")
     args = ap.parse_args()
     from hvamd import _lib
     if args.lib:
@@ -73,7 +81,7 @@ def main():
     lib = _lib.load()
     tot_f = tot_b = 0.0
     byt_f = byt_b = 0
-    for si, (name, B, H, W, C, nh, win, sh, nblk) in enumerate(STAGES):
+    for si, (name, B, H, W, C, nh, win, sh, nblk) in enumerate(STAGES_B384 if args.b384 else STAGES):
         if args.stage is not None and si != args.stage:
             continue
         T = B * H * W
