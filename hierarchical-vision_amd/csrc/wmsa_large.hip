@@ -19,17 +19,13 @@
 // bank-conflict free (checked with the LDS bank model of MI355X_MICROARCH.md).
 #include "wmsa_common.h"
 
-// experiment builds (not the product): 1 no CPB-gradient LDS atomics, 2 also no CPB gathers
+// experiment build (not the product): 1 no CPB-gradient accumulation
 #ifndef HVK_LARGE_PROBE
 #define HVK_LARGE_PROBE 0
 #endif
 #ifndef HVK_LARGE_BINS
 #define HVK_LARGE_BINS 1
 #endif
-#ifndef HVK_LARGE_QSTRIDE
-#define HVK_LARGE_QSTRIDE 1
-#endif
-#define LTAB(i) (HVK_LARGE_PROBE >= 2 ? 0.f : tab[i])
 
 namespace hvk_wmsa {
 namespace {
@@ -54,6 +50,12 @@ struct LCfg {
   static constexpr int BWAVES = HVK_LARGE_BINS ? 8 : WAVES;
   static constexpr int BTHREADS = 64 * BWAVES;
   static constexpr int RRP = (RR + 3) / 4 * 4;  // bins per copy (16-B aligned)
+  // mirrored CPB table: entry j = RR - 1 - (bq - bk), so the 4 consecutive keys 4g .. 4g+3 of
+  // a lane (one window row: 4 | WIN) read 4 ascending floats (two ds_read2_b32) straight into
+  // the MFMA C operand; padding keys (w12's last chunk) index past RR into zeros
+  static constexpr int QBMIN = (WIN - 1) * R + WIN - 1;
+  static constexpr int KBMAX = ((ROWS - 1) / WIN) * R + (ROWS - 1) % WIN;
+  static constexpr int TABM = ((RR - QBMIN + KBMAX > RR ? RR - QBMIN + KBMAX : RR) + 4) / 4 * 4;
 };
 
 // X^T fragment (A operand) of the 32-row chunk c, head-dim half dt, from an image of X
@@ -79,15 +81,13 @@ __device__ __forceinline__ PosInfo<WIN> key_info(int pos, int lim) {
   const int ph = pos / WIN, pw = pos - ph * WIN;
   return {ph * LCfg<WIN>::R + pw, ph >= lim, pw >= lim};
 }
-// the -100 shift-region mask of (key, query) as a select, not a branch on the (uniform) edge
-// flags: a branch over the mask code left its MFMA-result reader too close (hvk_common.h hvk_settle)
-template <int WIN>
-__device__ __forceinline__ float mask_of(bool edge_r, bool edge_c, const PosInfo<WIN>& k,
-                                         const PosInfo<WIN>& q, float mask2) {
-  return ((edge_r & (k.r != q.r)) | (edge_c & (k.c != q.c))) ? mask2 : 0.f;
-}
-
 // ------------------------------------------------------------------------------ forward
+// Per query tile (query on the lane), keys in 32-key chunks: S' = K^ (scale log2e Q^)^T +
+// (log2e bias - M_h) with the mirrored bias table as the MFMA C operand, M_h = scale log2e +
+// max bias the head bound of every logit (as the ring kernel, wmsa_ring.hip), so the fast path
+// exponentiates S' directly -- no running max, no rescaling -- and checks the row sums at the
+// end: a tile where any row sum fell below 2^-100 (a row far below the head bound, scale ~100)
+// is recomputed with the true running max (the reference's softmax, swinv2.py:256).
 template <int WIN>
 __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(FwdArgs a) {
   using K = LCfg<WIN>;
@@ -98,14 +98,20 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
   if (w >= g.n_windows) return;
   char* kimg = smem;
   char* vimg = smem + K::IMG;
-  float* tab = reinterpret_cast<float*>(smem + 2 * K::IMG);
+  float* mtab = reinterpret_cast<float*>(smem + 2 * K::IMG);
+  float* red = mtab + K::TABM;  // [WAVES] max-bias partials
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   const int C = g.C, C3 = 3 * C;
   const int per_img = g.nWh * g.nWw;
   const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+  const float sc2 = a.scale[h] * HVK_LOG2E;
 
   const float* bsrc = a.bias + (size_t)h * K::RR;
-  for (int e = threadIdx.x; e < K::RR; e += K::THREADS) tab[e] = bsrc[e] * HVK_LOG2E;
+  float mb = -INFINITY;
+  for (int e = threadIdx.x; e < K::RR; e += K::THREADS) mb = fmaxf(mb, bsrc[e]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
+  if (lane == 0) red[wave] = mb;
   // stage k^ (natural fragments) and v (head_dim permuted for 16-B output stores, as in
   // wmsa.hip: col 16dt + 4g + r <-> d = 8g + 4dt + r)
   for (int t = wave; t < 2 * K::NC; t += K::WAVES) {
@@ -123,92 +129,128 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
     *reinterpret_cast<uint2*>(vimg + fm8(pos, 4 + gq)) = make_uint2(vv.z, vv.w);
   }
   __syncthreads();
+  float Mh = red[0];
+#pragma unroll
+  for (int i = 1; i < K::WAVES; ++i) Mh = fmaxf(Mh, red[i]);
+  Mh = Mh * HVK_LOG2E + sc2;
+  for (int e = threadIdx.x; e < K::TABM; e += K::THREADS) {
+    const int i = K::RR - 1 - e;
+    mtab[e] = i >= 0 ? bsrc[i] * HVK_LOG2E - Mh : 0.f;
+  }
+  __syncthreads();
 
-  const float sc2 = a.scale[h] * HVK_LOG2E;
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
+  const bool edge = g.shift && (wh == g.nWh - 1 || ww == g.nWw - 1);
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
 
   for (int t0 = wave * K::QB; t0 < K::NT; t0 += K::WAVES * K::QB) {
     uint4 qf[K::QB];
     int qrow[K::QB];
     PosInfo<WIN> qi[K::QB];
-    float m[K::QB], l[K::QB];
     hvk_f32x4 o[K::QB][2];
+    float l[K::QB];
 #pragma unroll
     for (int j = 0; j < K::QB; ++j) {
-      const int pos = 16 * (t0 + j) + li, posc = pos < K::N ? pos : K::N - 1;
-      qrow[j] = window_token_row(g, b, wh, ww, WIN, posc);
-      qf[j] = pos < K::N ? hvk_ld16(a.qkv + (size_t)qrow[j] * C3 + h * 32 + 8 * gq) : make_uint4(0, 0, 0, 0);
+      const int pos = 16 * (t0 + j) + li;
+      qrow[j] = window_token_row(g, b, wh, ww, WIN, pos);
+      qf[j] = hvk_ld16(a.qkv + (size_t)qrow[j] * C3 + h * 32 + 8 * gq);
       float rn;
       qf[j] = l2_normalize(qf[j], rn, sc2);  // q^ * scale * log2e
-      qi[j] = query_info<WIN>(posc, lim);
-      m[j] = -INFINITY;
+      qi[j] = query_info<WIN>(pos, lim);
+    }
+    // S' of (key chunk c, half t, query tile j), masked; padding keys -inf
+    auto scores = [&](int c, int t, int j, const uint4& kf) {
+      const int kp = 32 * c + 16 * t + 4 * gq;  // this lane's 4 keys kp .. kp + 3 (one row)
+      const int ky = kp / WIN, kx = kp - ky * WIN;
+      const float* tp = mtab + (K::RR - 1 - qi[j].b + ky * K::R + kx);
+      hvk_f32x4 s = hvk_mfma16(kf, qf[j], hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
+      hvk_settle(s);  // the unmasked path branches over the mask code to its readers
+      if (edge) {  // wave-uniform: last window row / column of a shifted block only
+        const bool rmis = edge_r && ((ky >= lim) != qi[j].r);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool cmis = edge_c && ((kx + r >= lim) != qi[j].c);
+          s[r] += (rmis || cmis) ? mask2 : 0.f;
+        }
+      }
+      if (K::N % 32 != 0 && c == K::NC - 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kp + r >= K::N) s[r] = -INFINITY;
+      }
+      return s;
+    };
+#pragma unroll
+    for (int j = 0; j < K::QB; ++j) {
       l[j] = 0.f;
       o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
     }
-#pragma unroll 1
+#pragma unroll 3
     for (int c = 0; c < K::NC; ++c) {
       const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
       const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
       const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
-      PosInfo<WIN> ki[2][4];
-      bool kpad[2][4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 32 * c + 16 * t + 4 * gq + r;
-          kpad[t][r] = key >= K::N;
-          ki[t][r] = key_info<WIN>(kpad[t][r] ? K::N - 1 : key, lim);
-        }
 #pragma unroll
       for (int j = 0; j < K::QB; ++j) {
-        hvk_f32x4 s[2] = {hvk_mfma16(kf0, qf[j], hvk_f32x4{0, 0, 0, 0}),
-                          hvk_mfma16(kf1, qf[j], hvk_f32x4{0, 0, 0, 0})};
-        float mc = -INFINITY;
+        hvk_f32x4 s0 = scores(c, 0, j, kf0), s1 = scores(c, 1, j, kf1);
+        float p[8];
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = s[t][r] + LTAB(qi[j].b - ki[t][r].b);
-            v += mask_of(edge_r, edge_c, ki[t][r], qi[j], mask2);
-            if (kpad[t][r]) v = -INFINITY;
-            s[t][r] = v;
-            mc = fmaxf(mc, v);
-          }
-        mc = hvk_group4_max(mc);
-        const float mn = fmaxf(m[j], mc);
-        const float alpha = __builtin_amdgcn_exp2f(m[j] - mn);
-        m[j] = mn;
-        float ps = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s[t][r] = __builtin_amdgcn_exp2f(s[t][r] - mn);
-            ps += s[t][r];
-          }
-        l[j] = l[j] * alpha + ps;
-        o[j][0] *= alpha;
-        o[j][1] *= alpha;
-        const uint4 pf = make_uint4(hvk_pack2(s[0][0], s[0][1]), hvk_pack2(s[0][2], s[0][3]),
-                                    hvk_pack2(s[1][0], s[1][1]), hvk_pack2(s[1][2], s[1][3]));
+        for (int r = 0; r < 4; ++r) {
+          p[r] = __builtin_amdgcn_exp2f(s0[r]);
+          p[4 + r] = __builtin_amdgcn_exp2f(s1[r]);
+        }
+        l[j] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+        const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                    hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
         o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
         o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
       }
     }
 #pragma unroll
     for (int j = 0; j < K::QB; ++j) {
-      const int pos = 16 * (t0 + j) + li;
-      const float inv = __builtin_amdgcn_rcpf(hvk_group4_sum(l[j]));
-      if (pos < K::N) {
-        const uint4 pk = make_uint4(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv),
-                                    hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv),
-                                    hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv),
-                                    hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv));
-        hvk_st16(a.out + (size_t)qrow[j] * C + h * 32 + 8 * gq, pk);
+      l[j] = hvk_group4_sum(l[j]);
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l[j] >= 0x1p-100f)) != 0, 0)) {
+        // slow path (rare, wave-uniform): this tile again with the true running max
+        float m = -INFINITY;
+        l[j] = 0.f;
+        o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll 1
+        for (int c = 0; c < K::NC; ++c) {
+          const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
+          const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
+          const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+          hvk_f32x4 s0 = scores(c, 0, j, kf0), s1 = scores(c, 1, j, kf1);
+          float mc = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s0[r], s1[r]));
+          mc = hvk_group4_max(mc);
+          const float mn = fmaxf(m, mc);
+          const float alpha = __builtin_amdgcn_exp2f(m - mn);
+          m = mn;
+          float p[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
+            p[4 + r] = __builtin_amdgcn_exp2f(s1[r] - mn);
+          }
+          l[j] = l[j] * alpha + ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          o[j][0] *= alpha;
+          o[j][1] *= alpha;
+          const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                      hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+          o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
+          o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
+        }
+        l[j] = hvk_group4_sum(l[j]);
+        hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
       }
+      const float inv = __builtin_amdgcn_rcpf(l[j]);
+      const uint4 pk = make_uint4(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv),
+                                  hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv),
+                                  hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv),
+                                  hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv));
+      hvk_st16(a.out + (size_t)qrow[j] * C + h * 32 + 8 * gq, pk);
     }
   }
 }
@@ -252,9 +294,15 @@ template <int WIN>
 constexpr size_t bwd_large_lds() {
   using K = LCfg<WIN>;
   const size_t bins = HVK_LARGE_BINS ? (size_t)K::BWAVES * K::RRP : (size_t)K::RR;
-  return 2 * (size_t)K::IMG + (size_t)K::RRP * 4 + bins * 4 + 2 * (size_t)K::ROWS * 4;
+  return 2 * (size_t)K::IMG + (size_t)K::TABM * 4 + bins * 4 + 2 * (size_t)K::ROWS * 4 + 64;
 }
 
+// Logits relative to the head bound, as the forward: S' = sc2 cos + log2e bias - M_h from one
+// MFMA with the mirrored CPB table as its C operand (4 ascending floats for the lane's 4
+// consecutive keys in phase 1; 4 descending for its 4 consecutive queries in phase 2), plus
+// the -100 mask on edge windows (wave-uniform branch).  Phase 1 loop A exponentiates S'
+// directly (S' <= 0) and falls back to a running row max only for a tile whose row sum
+// underflows; the row constants kept for loop B and phase 2 are relative to M_h.
 template <int WIN>
 __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(BwdArgs a) {
   using K = LCfg<WIN>;
@@ -265,11 +313,12 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
   if (w >= g.n_windows) return;
   char* img0 = smem;
   char* img1 = smem + K::IMG;
-  float* tab = reinterpret_cast<float*>(smem + 2 * K::IMG);
-  float* dtab = tab + K::RRP;    // [BWAVES][RRP] private bins (HVK_LARGE_BINS) or [RR] shared
+  float* mtab = reinterpret_cast<float*>(smem + 2 * K::IMG);  // [TABM] mirrored, - M_h
+  float* dtab = mtab + K::TABM;  // [BWAVES][RRP] private bins (HVK_LARGE_BINS) or [RR] shared
   constexpr int NBIN = HVK_LARGE_BINS ? K::BWAVES * K::RRP : K::RR;
-  float* lse_s = dtab + NBIN;    // [ROWS] row log2-sum-exp2 (+inf for padding rows)
+  float* lse_s = dtab + NBIN;    // [ROWS] row constant relative to M_h (+inf: padding rows)
   float* dlt_s = lse_s + K::ROWS;  // [ROWS] delta = rowsum(P * dP)
+  float* red = dlt_s + K::ROWS;  // [16] max-bias partials
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   const int C = g.C, C3 = 3 * C;
   const int per_img = g.nWh * g.nWw;
@@ -279,9 +328,14 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+  const bool edge = HVK_LARGE_PROBE == 3 ? false : (edge_r || edge_c);  // probe 3: no mask (not exact)
 
   const float* bsrc = a.bias + (size_t)h * K::RR;
-  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) tab[e] = bsrc[e] * HVK_LOG2E;
+  float mb = -INFINITY;
+  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) mb = fmaxf(mb, bsrc[e]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
+  if (lane == 0) red[wave] = mb;
   for (int e = threadIdx.x; e < NBIN; e += K::BTHREADS) dtab[e] = 0.f;
   for (int e = threadIdx.x; e < K::ROWS; e += K::BTHREADS) {
     lse_s[e] = INFINITY;
@@ -302,70 +356,110 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
     *reinterpret_cast<uint4*>(img1 + fm16(pos, gq)) = vv;
   }
   __syncthreads();
+  float Mh = red[0];
+#pragma unroll
+  for (int i = 1; i < K::BWAVES; ++i) Mh = fmaxf(Mh, red[i]);
+  Mh = Mh * HVK_LOG2E + sc2;
+  for (int e = threadIdx.x; e < K::TABM; e += K::BTHREADS) {
+    const int i = K::RR - 1 - e;
+    mtab[e] = i >= 0 ? bsrc[i] * HVK_LOG2E - Mh : 0.f;
+  }
+  __syncthreads();
 
   // ---------------- phase 1: query tiles (query on the lane)
   float dscale = 0.f;
   float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   for (int qt = wave; qt < K::NT; qt += K::BWAVES) {
     // query tile qt = positions qt + NT*li (N = 16 NT for w 12/16/24): the 16 queries of a tile
-    // lie >= one window row apart, so the CPB-gradient atomics of one instruction (query li,
-    // key 4g + r) never share an LDS address (consecutive queries put 4 lanes on each)
-    const int pos = HVK_LARGE_QSTRIDE ? qt + K::NT * li : 16 * qt + li, posc = pos < K::N ? pos : K::N - 1;
-    const bool qvalid = pos < K::N;
-    const int qrow = window_token_row(g, b, wh, ww, WIN, posc);
+    // lie >= one window row apart, so the CPB-gradient bins of one read-add-write batch are
+    // distinct across the lanes (loop B)
+    const int pos = qt + K::NT * li;
+    const int qrow = window_token_row(g, b, wh, ww, WIN, pos);
     const hvk_bf16* qp = a.qkv + (size_t)qrow * C3 + h * 32;
-    const uint4 qraw = qvalid ? hvk_ld16(qp + 8 * gq) : make_uint4(0, 0, 0, 0);
-    const uint4 dof = qvalid ? hvk_ld16(a.dout + (size_t)qrow * C + h * 32 + 8 * gq) : make_uint4(0, 0, 0, 0);
+    const uint4 qraw = hvk_ld16(qp + 8 * gq);
+    const uint4 dof = hvk_ld16(a.dout + (size_t)qrow * C + h * 32 + 8 * gq);
     float rnq;
     const uint4 qs = l2_normalize(qraw, rnq, sc2);
-    const PosInfo<WIN> qi = query_info<WIN>(posc, lim);
+    const PosInfo<WIN> qi = query_info<WIN>(pos, lim);
+    const float* tq = mtab + (K::RR - 1 - qi.b);  // + kb(key) + r
 
-    // loop A: row max, sum and delta (online)
-    float m = -INFINITY, l = 0.f, dacc = 0.f;
-#pragma unroll 1
-    for (int c = 0; c < K::NC; ++c) {
-      float v[2][4], dp[2][4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int kt = 2 * c + t;
-        const hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(16 * kt + li, gq)), qs, hvk_f32x4{0, 0, 0, 0});
-        const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(16 * kt + li, gq)), dof, hvk_f32x4{0, 0, 0, 0});
+    // S' (masked; padding keys -inf) and dP - 0 of chunk c, half t; c4 = the bias C operand
+    auto tile = [&](int c, int t, hvk_f32x4& s, hvk_f32x4& d, hvk_f32x4& c4) {
+      const int kt = 2 * c + t, kp = 16 * kt + 4 * gq;
+      const int ky = kp / WIN, kx = kp - ky * WIN;
+      const float* tp = tq + ky * K::R + kx;
+      c4 = hvk_f32x4{tp[0], tp[1], tp[2], tp[3]};
+      s = hvk_mfma16(lds16(img0, fm16(16 * kt + li, gq)), qs, c4);
+      d = hvk_mfma16(lds16(img1, fm16(16 * kt + li, gq)), dof, hvk_f32x4{0, 0, 0, 0});
+      hvk_settle(s, d);  // the unmasked path branches over the mask code to their readers
+      if (edge) {  // wave-uniform; selects, not branches, per element
+        const bool rmis = edge_r && ((ky >= lim) != qi.r);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = 16 * kt + 4 * gq + r;
-          const PosInfo<WIN> ki = key_info<WIN>(key < K::N ? key : K::N - 1, lim);
-          float x = s[r] + LTAB(qi.b - ki.b);
-          x += mask_of(edge_r, edge_c, ki, qi, mask2);
-          v[t][r] = key < K::N ? x : -INFINITY;
-          dp[t][r] = d[r];
+          const bool cmis = edge_c && ((kx + r >= lim) != qi.c);
+          s[r] += (rmis || cmis) ? mask2 : 0.f;
         }
       }
-      float mc = -INFINITY;
+      if (K::N % 32 != 0 && c == K::NC - 1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int r = 0; r < 4; ++r)
+          if (kp + r >= K::N) s[r] = -INFINITY;
+      }
+    };
+
+    // loop A: row sum and delta against the head bound
+    float l = 0.f, dacc = 0.f, m = 0.f;
+#pragma unroll 1
+    for (int c = 0; c < K::NC; ++c) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mc = fmaxf(mc, v[t][r]);
-      mc = hvk_group4_max(mc);
-      const float mn = fmaxf(m, mc);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      float ps = 0.f, pd = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t) {
+        hvk_f32x4 s, d, c4;
+        tile(c, t, s, d, c4);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(v[t][r] - mn);
-          ps += p;
-          pd += p * dp[t][r];
+          const float p = __builtin_amdgcn_exp2f(s[r]);
+          l += p;
+          dacc = fmaf(p, d[r], dacc);
         }
-      l = l * alpha + ps;
-      dacc = dacc * alpha + pd;
+      }
     }
     l = hvk_group4_sum(l);
     dacc = hvk_group4_sum(dacc);
-    const float lse = m + __log2f(l);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
+      // slow path (rare, wave-uniform): row max, sum and delta with a running max
+      m = -INFINITY;
+      l = 0.f;
+      dacc = 0.f;
+#pragma unroll 1
+      for (int c = 0; c < K::NC; ++c) {
+        hvk_f32x4 s[2], d[2], c4;
+        tile(c, 0, s[0], d[0], c4);
+        tile(c, 1, s[1], d[1], c4);
+        float mc = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s[0][r], s[1][r]));
+        mc = hvk_group4_max(mc);
+        const float mn = fmaxf(m, mc);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+        m = mn;
+        float ps = 0.f, pd = 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = __builtin_amdgcn_exp2f(s[t][r] - mn);
+            ps += p;
+            pd = fmaf(p, d[t][r], pd);
+          }
+        l = l * alpha + ps;
+        dacc = dacc * alpha + pd;
+      }
+      l = hvk_group4_sum(l);
+      dacc = hvk_group4_sum(dacc);
+    }
+    const float lse = m + __log2f(l);  // relative to M_h
     const float delta = dacc / l;
-    if (gq == 0 && qvalid) {
+    if (gq == 0) {
       lse_s[pos] = lse;
       dlt_s[pos] = delta;
     }
@@ -375,40 +469,57 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
 #pragma unroll 1
     for (int c = 0; c < K::NC; ++c) {
       float ds[2][4];
+      int bidx[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int kt = 2 * c + t;
-        const hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(16 * kt + li, gq)), qs, hvk_f32x4{0, 0, 0, 0});
-        const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(16 * kt + li, gq)), dof, hvk_f32x4{0, 0, 0, 0});
+        hvk_f32x4 s, d, c4;
+        tile(c, t, s, d, c4);
+        const int kp = 32 * c + 16 * t + 4 * gq, ky = kp / WIN, kx = kp - ky * WIN;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = 16 * kt + 4 * gq + r;
-          const bool kvalid = key < K::N;
-          const PosInfo<WIN> ki = key_info<WIN>(kvalid ? key : K::N - 1, lim);
-          const int idx = qi.b - ki.b;
-          float x = s[r] + LTAB(idx);
-          x += mask_of(edge_r, edge_c, ki, qi, mask2);
-          const float p = kvalid ? __builtin_amdgcn_exp2f(x - lse) : 0.f;
+          const bool kvalid = kp + r < K::N;
+          const float p = __builtin_amdgcn_exp2f(s[r] - lse);  // padding keys: exp2(-inf) = 0
           const float dsv = p * (d[r] - delta);
           ds[t][r] = dsv;
-          if (kvalid && qvalid) {
-            if (HVK_LARGE_PROBE >= 1) {
-            } else if (HVK_LARGE_BINS) {
-              // this wave's own bins; the 64 lanes of one read-add-write never share a bin
-              // (strided query tiles), and a wave's LDS operations complete in order.  The
-              // compiler fences keep each read-add-write whole: without them hipcc merges the
-              // reads of a lane's adjacent bins (r, r + 1) ahead of the writes, which is
-              // exact per lane but loses the updates another lane makes in between
-              float* pb = dtab + wave * K::RRP + idx;
-              asm volatile("" ::: "memory");
-              *pb += dsv;
-              asm volatile("" ::: "memory");
-            } else {
-              atomicAdd(&dtab[idx], dsv);  // LDS float atomic (ds_add_f32)
-            }
-            dscale += dsv * s[r];        // s = sc2 * cos: divided out at the end
-          }
+          bidx[t][r] = qi.b - (ky * K::R + kx + r);
+          if (kvalid) dscale += dsv * (s[r] - c4[r]);  // sc2 * cos (the mask only where p ~ 0)
         }
+      }
+      // CPB-table gradient: this wave's own bins (plain LDS read-add-write, no float atomics).
+      // A batch of read-add-writes is exact when no two of its (lane, element) pairs share a
+      // bin: with the strided query tiles that holds for a whole 32-key chunk at w24, for each
+      // 16-key half at w16, per element at w12 (tools/large_bins_check.py); LDS operations of a
+      // wave complete in order, and the compiler fences keep hipcc from merging the reads of
+      // one batch ahead of another's writes (exact per lane, but it loses other lanes' updates)
+      if (HVK_LARGE_PROBE >= 1) {
+      } else if (HVK_LARGE_BINS) {
+        float* pb = dtab + wave * K::RRP;
+        constexpr int BATCH = WIN == 24 ? 8 : (WIN == 16 ? 4 : 1);
+#pragma unroll
+        for (int b0 = 0; b0 < 8; b0 += BATCH) {
+          float v[BATCH];
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int e = 0; e < BATCH; ++e) {
+            const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
+            const bool ok = 32 * c + 16 * t + 4 * gq + r < K::N;
+            v[e] = ok ? pb[bidx[t][r]] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < BATCH; ++e) {
+            const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
+            const bool ok = 32 * c + 16 * t + 4 * gq + r < K::N;
+            if (ok) pb[bidx[t][r]] = v[e] + ds[t][r];
+          }
+          asm volatile("" ::: "memory");
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (32 * c + 16 * t + 4 * gq + r < K::N)
+              atomicAdd(&dtab[bidx[t][r]], ds[t][r]);  // LDS float atomic (ds_add_f32)
       }
       const uint4 bf = make_uint4(hvk_pack2(scale * ds[0][0], scale * ds[0][1]),
                                   hvk_pack2(scale * ds[0][2], scale * ds[0][3]),
@@ -417,8 +528,7 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
       dq[0] = hvk_mfma16(tr_frag(img0, c, 0, li, gq), bf, dq[0]);
       dq[1] = hvk_mfma16(tr_frag(img0, c, 1, li, gq), bf, dq[1]);
     }
-    normalize_bwd_store(qp, rnq, dq, qvalid ? a.dqkv + (size_t)qrow * C3 + h * 32 : nullptr,
-                        1.f, gq, dqb);
+    normalize_bwd_store(qp, rnq, dq, a.dqkv + (size_t)qrow * C3 + h * 32, 1.f, gq, dqb);
   }
   __syncthreads();
 
@@ -440,34 +550,47 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
 
   // ---------------- phase 2: key tiles (key on the lane)
   for (int kt = wave; kt < K::NT; kt += K::BWAVES) {
-    const int pos = 16 * kt + li, posc = pos < K::N ? pos : K::N - 1;
-    const bool kvalid = pos < K::N;
-    const int krow = window_token_row(g, b, wh, ww, WIN, posc);
+    const int pos = 16 * kt + li;
+    const int krow = window_token_row(g, b, wh, ww, WIN, pos);
     const hvk_bf16* kp = a.qkv + (size_t)krow * C3 + h * 32 + C;
-    const uint4 kraw = kvalid ? hvk_ld16(kp + 8 * gq) : make_uint4(0, 0, 0, 0);
-    const uint4 vf = kvalid ? hvk_ld16(kp + C + 8 * gq) : make_uint4(0, 0, 0, 0);
+    const uint4 kraw = hvk_ld16(kp + 8 * gq);
+    const uint4 vf = hvk_ld16(kp + C + 8 * gq);
     float rnk;
     const uint4 kh = l2_normalize(kraw, rnk);
-    const PosInfo<WIN> ki = key_info<WIN>(posc, lim);
+    const PosInfo<WIN> ki = key_info<WIN>(pos, lim);
+    const float* tk = mtab + (K::RR - 1 + ki.b);  // - qb(query)
     hvk_f32x4 dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll 1
     for (int c = 0; c < K::NC; ++c) {
       float p[2][4], ds[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int qt = 2 * c + t;
-        const hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(16 * qt + li, gq)), kh, hvk_f32x4{0, 0, 0, 0});
+        const int qt = 2 * c + t, q0 = 16 * qt + 4 * gq;  // this lane's queries q0 .. q0 + 3
+        if (K::NT % 2 == 1 && qt >= K::NT) {  // w12's padding half chunk: no queries
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[t][r] = ds[t][r] = 0.f;
+          continue;
+        }
+        const int qy = q0 / WIN, qx = q0 - qy * WIN;
+        const float* tp = tk - ((qy + WIN - 1) * K::R + qx + WIN - 1);  // entries tp[-r]
+        hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(16 * qt + li, gq)), kh,
+                                 hvk_f32x4{tp[0], tp[-1], tp[-2], tp[-3]});
         const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(16 * qt + li, gq)), vf, hvk_f32x4{0, 0, 0, 0});
-        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 16 * qt + 4 * gq);
-        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + 16 * qt + 4 * gq);
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
+        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);
         const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+        hvk_settle(s);
+        if (edge) {  // wave-uniform; selects, not branches, per element
+          const bool rmis = edge_r && (ki.r != (qy >= lim));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const bool cmis = edge_c && (ki.c != (qx + r >= lim));
+            s[r] += (rmis || cmis) ? mask2 : 0.f;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int q = 16 * qt + 4 * gq + r;
-          const PosInfo<WIN> qi = query_info<WIN>(q < K::N ? q : K::N - 1, lim);
-          float x = s[r] + LTAB(qi.b - ki.b);
-          x += mask_of(edge_r, edge_c, ki, qi, mask2);
-          p[t][r] = __builtin_amdgcn_exp2f(x - lr[r]);  // padding query: lse = +inf -> 0
+          p[t][r] = __builtin_amdgcn_exp2f(s[r] - lr[r]);  // padding query: lse = +inf -> 0
           ds[t][r] = p[t][r] * (d[r] - dr[r]);
         }
       }
@@ -483,13 +606,11 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
     }
     // dk^ = sum_q scale dS q^ = sum_q dS (q^ scale log2e) / log2e
     hvk_bf16* dst = a.dqkv + (size_t)krow * C3 + h * 32;
-    normalize_bwd_store(kp, rnk, dk, kvalid ? dst + C : nullptr, 1.f / HVK_LOG2E, gq, nullptr);
-    if (kvalid) {
+    normalize_bwd_store(kp, rnk, dk, dst + C, 1.f / HVK_LOG2E, gq, nullptr);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-        hvk_st8(dst + 2 * C + 16 * dt + 4 * gq,
-                make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
-    }
+    for (int dt = 0; dt < 2; ++dt)
+      hvk_st8(dst + 2 * C + 16 * dt + 4 * gq,
+              make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
   }
   __syncthreads();
 
@@ -529,7 +650,7 @@ __global__ __launch_bounds__(256) void wmsa_finalize_large_kernel(BwdArgs a, flo
 template <int WIN>
 int launch_fwd_large(const FwdArgs& a, hipStream_t st) {
   using K = LCfg<WIN>;
-  const size_t lds = 2 * (size_t)K::IMG + (size_t)K::RR * 4;
+  const size_t lds = 2 * (size_t)K::IMG + ((size_t)K::TABM + K::WAVES) * 4;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_large_kernel<WIN>),
