@@ -15,8 +15,11 @@ block is re-planned around the hardware:
   window_reverse (swinv2.py:69-102, 399-429) never materialise.
 * Post-norm + DropPath + residual add is one kernel (``ops.layer_norm_residual``).
 * PatchMerging's strided 2x2 gather is one kernel (``ops.patch_merge_gather``).
-* Dense contractions (qkv, proj, fc1, fc2, reduction, patch embedding, head)
-  are plain library GEMMs (hipBLASLt via torch) in bf16 under autocast.
+* Dense contractions (qkv, proj, fc1, fc2, reduction, patch embedding) run on
+  libhvk's MFMA GEMMs in bf16 under autocast (``ops.linear``: the skinny
+  weight-stationary kernel at the SwinV2-T stage 0-1 widths, the tiled kernel
+  elsewhere, the weight-gradient kernel for every weight and bias gradient); only
+  the classifier / multitask heads (M = batch) stay on hipBLASLt via torch.
 """
 import dataclasses
 import os

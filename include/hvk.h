@@ -79,7 +79,8 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
  * y[M, N] = x[M, K] w[N, K]^T (+ bias[N]), bf16 in/out, f32 accumulation: F.linear of
  * swinv2.py:58-62 (fc1/fc2), 220 (qkv), 262 (proj), 492 (PatchMerging.reduction) and
  * 652 (patch embedding as GEMM) for the (K, N) shapes hvk_linear_supported() reports
- * (SwinV2-T/B stages 0-1); with w = weight^T it is the input gradient of those layers.
+ * (the SwinV2-T stage 0-1 widths; other widths, e.g. SwinV2-B's C = 128 / 256, run on the tiled
+ * hvk_gemm_fwd); with w = weight^T it is the input gradient of those layers.
  * x: bf16 [M, K]; w: bf16 [N, K]; bias: f32 [N] or NULL; y: bf16 [M, N]. */
 int hvk_linear_supported(int M, int K, int N);
 int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N,
