@@ -17,16 +17,21 @@ HBM = 5.5e12
 MFMA = 2.5e15
 B = 256
 STAGES = [(802816, 96, 2), (200704, 192, 2), (50176, 384, 6), (12544, 768, 2)]  # T, C, blocks
+MODELS = {
+    "t": STAGES,  # SwinV2-T 224 (config 3)
+    "b224": [(802816, 128, 2), (200704, 256, 2), (50176, 512, 18), (12544, 1024, 2)],  # config 4
+    "b384": [(2359296, 128, 2), (589824, 256, 2), (147456, 512, 18), (36864, 1024, 2)],  # config 5
+}
 
 
-def shapes():
+def shapes(model="t"):
     out = []  # (name, M, K, N, count per step)
-    for s, (T, C, nb) in enumerate(STAGES):
+    for s, (T, C, nb) in enumerate(MODELS[model]):
         out += [(f"s{s}.qkv", T, C, 3 * C, nb), (f"s{s}.proj", T, C, C, nb),
                 (f"s{s}.fc1", T, C, 4 * C, nb), (f"s{s}.fc2", T, 4 * C, C, nb)]
         if s < 3:
             out.append((f"s{s}.merge", T // 4, 4 * C, 2 * C, 1))
-    out.append(("embed", B * 3136, 48, 96, 1))
+    out.append(("embed", MODELS[model][0][0], 48, MODELS[model][0][1], 1))
     out.append(("head", B, 768, 10000, 1))
     return out
 
@@ -50,6 +55,7 @@ def main():
     ap.add_argument("--tunable", default=None, help="enable PyTorch TunableOp, results file path")
     ap.add_argument("--only", default=None, help="regex of gemm names to run")
     ap.add_argument("--lib", default=None, help="load this libhvk build instead (tools/probe)")
+    ap.add_argument("--model", default="t", choices=sorted(MODELS), help="stage shapes: t, b224, b384")
     a = ap.parse_args()
     if a.lib:
         from hvamd import _lib as L
@@ -67,7 +73,7 @@ def main():
     tot_h = 0.0
     print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw | hvk fwd/dx us | tile fwd/dx us")
     import re
-    for name, M, K, N, cnt in shapes():
+    for name, M, K, N, cnt in shapes(a.model):
         if a.only and not re.search(a.only, name):
             continue
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
