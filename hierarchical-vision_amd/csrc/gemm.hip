@@ -274,6 +274,15 @@ const LinCfg kLin[][4] = {
     // stage 2 fc2 input gradient with the GELU backward (EPI 2); plain stage-2 GEMMs run on the
     // tiled kernel (gemm_tile.hip)
     {{384, 1536, 128, 8, 1}, {384, 1536, 64, 8, 1}, {384, 1536, 128, 8, 1}, {384, 1536, 64, 4, 1}},
+    // SwinV2-B stages 0-1 (C = 128, 256) and its patch embedding; fc1 (N = 4C) also as the
+    // fused GELU epilogues (hvk_linear_gelu_fwd / _bwd)
+    {{48, 128, 128, 8, 1}, {48, 128, 128, 16, 1}, {48, 128, 128, 16, 0}, {48, 128, 128, 8, 1}},
+    {{128, 128, 128, 8, 1}, {128, 128, 128, 16, 1}, {128, 128, 128, 16, 0}, {128, 128, 128, 8, 1}},
+    {{128, 384, 192, 8, 1}, {128, 384, 192, 16, 1}, {128, 384, 192, 16, 0}, {128, 384, 128, 8, 1}},
+    {{128, 512, 256, 8, 1}, {128, 512, 256, 16, 1}, {128, 512, 256, 16, 0}, {128, 512, 128, 8, 1}},
+    {{256, 256, 128, 8, 1}, {256, 256, 128, 16, 1}, {256, 256, 128, 16, 0}, {256, 256, 128, 8, 1}},
+    {{256, 768, 128, 8, 1}, {256, 768, 128, 16, 1}, {256, 768, 128, 16, 0}, {256, 768, 128, 8, 1}},
+    {{256, 1024, 128, 8, 1}, {256, 1024, 128, 16, 1}, {256, 1024, 128, 16, 0}, {256, 1024, 128, 8, 1}},
 };
 
 const LinCfg* pick(int K, int N) {
@@ -311,6 +320,7 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
   HVK_LIN3(288, 96) HVK_LIN3(192, 192) HVK_LIN3(192, 288) HVK_LIN3(192, 256) HVK_LIN3(384, 192)
   HVK_LIN(96, 192, 16, 1) HVK_LIN(384, 96, 8, 0) HVK_LIN(288, 96, 8, 0) HVK_LIN(192, 96, 16, 1)
   HVK_LIN(384, 96, 16, 1) HVK_LIN(384, 128, 8, 1) HVK_LIN(384, 64, 8, 1) HVK_LIN(384, 64, 4, 1)
+  HVK_LIN3(48, 128) HVK_LIN3(128, 128) HVK_LIN3(128, 192) HVK_LIN3(128, 256) HVK_LIN3(256, 128)
 #undef HVK_LIN3
 #undef HVK_LIN
   return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);
@@ -319,7 +329,8 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
 int hvk_linear_gelu_supported(int M, int K, int N) {
   const LinCfg* c = pick(K, N);
   return M > 0 && c &&
-         ((c->K == 96 && c->BN == 384) || (c->K == 192 && c->BN == 256) || (c->K == 384 && c->BN == 128)) &&
+         ((c->K == 96 && c->BN == 384) || (c->K == 192 && c->BN == 256) || (c->K == 384 && c->BN == 128) ||
+          (c->K == 128 && c->BN == 256) || (c->K == 256 && c->BN == 128)) &&
          c->N == 4 * c->K && c->waves == 8 && c->pref == 1;
 }
 
@@ -335,6 +346,8 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   hvk_bf16* Yg = static_cast<hvk_bf16*>(y);
   if (K == 96) return launch_linear<96, 384, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   if (K == 384) return launch_linear<384, 128, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+  if (K == 128) return launch_linear<128, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+  if (K == 256) return launch_linear<256, 128, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
 }
 
@@ -351,7 +364,8 @@ int hvk_linear_gelu_in_fwd(const void* h, const void* w, const float* bias, void
 }
 
 int hvk_linear_gelu_bwd_supported(int M, int K, int N) {
-  return M > 0 && ((K == 96 && N == 384) || (K == 192 && N == 768) || (K == 384 && N == 1536));
+  return M > 0 && ((K == 96 && N == 384) || (K == 192 && N == 768) || (K == 384 && N == 1536) ||
+                   (K == 128 && N == 512) || (K == 256 && N == 1024));
 }
 
 int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, float* dbias,
@@ -367,6 +381,8 @@ int hvk_linear_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, 
   hvk_bf16* G = static_cast<hvk_bf16*>(gh);
   if (K == 96) return launch_linear<96, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
   if (K == 384) return launch_linear<384, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
+  if (K == 128) return launch_linear<128, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
+  if (K == 256) return launch_linear<256, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
   return launch_linear<192, 128, 8, true, 2>(X, W, nullptr, G, M, N, st, H, dbias);
 }
 

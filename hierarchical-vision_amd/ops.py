@@ -222,7 +222,7 @@ def gelu_fwd(x2, wb, bias):
     M, K = x2.shape
     N = wb.shape[0]
     lib = _lib.load()
-    if K in (96, 192) and lib.hvk_linear_gelu_supported(M, K, N):
+    if (K in (96, 192) or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N):
         fn = "hvk_linear_gelu_fwd"
     elif _tile_ok(M, K, N):
         fn = "hvk_gemm_gelu_fwd"
@@ -234,13 +234,21 @@ def gelu_fwd(x2, wb, bias):
     return h, y
 
 
+# SwinV2-B's stage 0-1 widths (K = 128 / 256): the skinny kernel before the tiled one
+_SKINNY_FIRST = {128, 256} if os.environ.get("HVK_SKINNY_B", "1") != "0" else set()
+
+
+def _skinny_first(M, K, N):
+    return K in _SKINNY_FIRST and _linear_native(M, K, N)
+
+
 def mm_nt(x2, wb, bias=None):
     """y = x2 wb^T (+ bias): libhvk's MFMA kernels where built (skinny weight-stationary for
     the memory-bound stage 0-1 shapes, tiled for stage 2), else the library GEMM.  x2 [M, K]
     bf16, wb [N, K] bf16, bias f32 [N]."""
     M, K = x2.shape
     N = wb.shape[0]
-    if _tile_ok(M, K, N):
+    if _tile_ok(M, K, N) and not _skinny_first(M, K, N):
         y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
         b = _f32(bias) if bias is not None else None
         call("hvk_gemm_fwd", ptr(x2), ptr(wb), ptr(b) if b is not None else None, ptr(y), M, K, N,
@@ -693,8 +701,8 @@ def linear_gelu(x, weight, bias):
     """GELU(F.linear(x, weight, bias)): fused kernel where built, else GEMM + activation kernel."""
     N, K = weight.shape
     M = x.numel() // K
-    if bias is not None and ((K in (96, 192) and _lib.load().hvk_linear_gelu_supported(M, K, N))
-                             or _tile_ok(M, K, N)):
+    if bias is not None and (((K in (96, 192) or K in _SKINNY_FIRST)
+                              and _lib.load().hvk_linear_gelu_supported(M, K, N)) or _tile_ok(M, K, N)):
         return LinearGelu.apply(x, weight, bias)
     return bias_gelu(linear(x, weight), bias)
 
@@ -748,7 +756,8 @@ class MlpFn(torch.autograd.Function):
             dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
         w2t = _bf16_t(w2b, ctx.wts[1])
-        if _tile_ok(M, N2, N1):
+        if _tile_ok(M, N2, N1) and not (N2 in _SKINNY_FIRST and
+                                         _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
             call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
         else:
             call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1,
@@ -767,7 +776,7 @@ def mlp(x, w1, b1, w2, b2=None):
     N1, K = w1.shape
     M = x.numel() // K
     lib = _lib.load()
-    if (b1 is not None and ((K in (96, 192) and lib.hvk_linear_gelu_supported(M, K, N1))
+    if (b1 is not None and (((K in (96, 192) or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N1))
                             or _tile_ok(M, K, N1))
             and (lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1) or _tile_ok(M, w2.shape[0], N1))):
         return MlpFn.apply(x, w1, b1, w2, b2)

@@ -5,7 +5,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(48, 96), (96, 96), (96, 288), (96, 384), (384, 96), (288, 96), (192, 192), (192, 576),
-          (192, 768), (384, 192), (384, 1536)]
+          (192, 768), (384, 192), (384, 1536),
+          # SwinV2-B stages 0-1 (C = 128, 256) and its patch embedding
+          (48, 128), (128, 128), (128, 384), (128, 512), (256, 256), (256, 768), (256, 1024)]
 
 
 @pytest.mark.parametrize("K,N", SHAPES)
@@ -45,7 +47,7 @@ def test_linear_autograd_uses_native_and_matches():
         assert rel < 1e-2, rel
 
 
-@pytest.mark.parametrize("K,N", [(96, 384), (192, 768), (384, 1536)])
+@pytest.mark.parametrize("K,N", [(96, 384), (192, 768), (384, 1536), (128, 512), (256, 1024)])
 def test_linear_gelu_fused_matches_fp32(K, N):
     from hvamd import _lib, ops
     M = 3000 if K < 384 else 40000
@@ -95,14 +97,14 @@ def test_mlp_gelu_recompute_bit_identical(monkeypatch, with_b2):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("C", [96, 192, 384, 768])
+@pytest.mark.parametrize("C", [96, 192, 384, 768, 128, 256])
 @pytest.mark.parametrize("with_b2", [False, True])
 def test_mlp_fused_backward_matches_fp32(C, with_b2):
     """fc2(GELU(fc1 x)) through the fused kernels (hvk_linear_gelu_fwd / _bwd, the tiled
     hvk_gemm_gelu_fwd / _bwd at stage 2-3) vs an fp32 autograd of the same bf16 operands:
     output, dx, dW1, db1, dW2, db2."""
     from hvamd import _lib, ops
-    M, N1 = {96: 3000, 192: 3000, 384: 40000, 768: 12544}[C], 4 * C  # stage 2: tiled at M >= 32768
+    M, N1 = {96: 3000, 192: 3000, 384: 40000, 768: 12544, 128: 40000, 256: 40000}[C], 4 * C  # stage 2: tiled at M >= 32768
     assert _lib.load().hvk_linear_gelu_bwd_supported(M, C, N1) or ops._tile_ok(M, C, N1)
     gen = torch.Generator(device="cuda").manual_seed(C)
     x = torch.randn(M, C, device="cuda", generator=gen).bfloat16().requires_grad_(True)
