@@ -651,7 +651,7 @@ int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table
   a.out = static_cast<hvk_bf16*>(out);
   a.bias = bias_table;
   a.scale = scale;
-  a.lse = hvk_wmsa::large_window(window) ? nullptr : lse;  // the large-window backward recomputes
+  a.lse = lse;
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hvk_wmsa::large_window(window)) {
     int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);

@@ -19,7 +19,8 @@
 // bank-conflict free (checked with the LDS bank model of MI355X_MICROARCH.md).
 #include "wmsa_common.h"
 
-// experiment build (not the product): 1 no CPB-gradient accumulation
+// experiment builds (not the product): 1 no CPB-gradient accumulation, 3 no edge masks,
+// 4 no phase 2, 5 no phase-1 loop B, 6 no phase-1 loop A
 #ifndef HVK_LARGE_PROBE
 #define HVK_LARGE_PROBE 0
 #endif
@@ -88,7 +89,7 @@ __device__ __forceinline__ PosInfo<WIN> key_info(int pos, int lim) {
 // exponentiates S' directly -- no running max, no rescaling -- and checks the row sums at the
 // end: a tile where any row sum fell below 2^-100 (a row far below the head bound, scale ~100)
 // is recomputed with the true running max (the reference's softmax, swinv2.py:256).
-template <int WIN>
+template <int WIN, bool LSE>
 __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(FwdArgs a) {
   using K = LCfg<WIN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
 #pragma unroll
     for (int j = 0; j < K::QB; ++j) {
       l[j] = hvk_group4_sum(l[j]);
+      float lshift = 0.f;  // the slow path's row max, on top of M_h
       if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l[j] >= 0x1p-100f)) != 0, 0)) {
         // slow path (rare, wave-uniform): this tile again with the true running max
         float m = -INFINITY;
@@ -243,8 +245,11 @@ __global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(F
           o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
         }
         l[j] = hvk_group4_sum(l[j]);
+        lshift = m;
         hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
       }
+      // LSE: the query's log2 row constant L2 = M_h + row max + log2(row sum) for the backward
+      if (LSE && gq == 0) a.lse[(size_t)qrow[j] * g.nH + h] = Mh + lshift + __log2f(l[j]);
       const float inv = __builtin_amdgcn_rcpf(l[j]);
       const uint4 pk = make_uint4(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv),
                                   hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv),
@@ -303,7 +308,7 @@ constexpr size_t bwd_large_lds() {
 // the -100 mask on edge windows (wave-uniform branch).  Phase 1 loop A exponentiates S'
 // directly (S' <= 0) and falls back to a running row max only for a tile whose row sum
 // underflows; the row constants kept for loop B and phase 2 are relative to M_h.
-template <int WIN>
+template <int WIN, bool LSE>
 __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(BwdArgs a) {
   using K = LCfg<WIN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -407,10 +412,23 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
       }
     };
 
+    // LSE: the forward's row constant and delta_O = dO . O from its output; loop B then
+    // measures how far its dS row sums miss zero and corrects delta, dQ and the logit-scale
+    // gradient exactly (the CPB gradient keeps the small remainder)
+    float lse_in = 0.f, dlt_o = 0.f;
+    if (LSE) {
+      lse_in = a.lse[(size_t)qrow * g.nH + h] - Mh;
+      float fd[8], fo[8];
+      hvk_unpack8(dof, fd);
+      hvk_unpack8(hvk_ld16(a.out + (size_t)qrow * C + h * 32 + 8 * gq), fo);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dlt_o = fmaf(fd[e], fo[e], dlt_o);
+      dlt_o = hvk_group4_sum(dlt_o);
+    }
     // loop A: row sum and delta against the head bound
-    float l = 0.f, dacc = 0.f, m = 0.f;
+    float l = HVK_LARGE_PROBE == 6 ? 1.f : 0.f, dacc = 0.f, m = 0.f;
 #pragma unroll 1
-    for (int c = 0; c < K::NC; ++c) {
+    for (int c = 0; c < (HVK_LARGE_PROBE == 6 || LSE ? 0 : K::NC); ++c) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         hvk_f32x4 s, d, c4;
@@ -425,7 +443,7 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
     }
     l = hvk_group4_sum(l);
     dacc = hvk_group4_sum(dacc);
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
+    if (!LSE && __builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
       // slow path (rare, wave-uniform): row max, sum and delta with a running max
       m = -INFINITY;
       l = 0.f;
@@ -457,18 +475,15 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
       l = hvk_group4_sum(l);
       dacc = hvk_group4_sum(dacc);
     }
-    const float lse = m + __log2f(l);  // relative to M_h
-    const float delta = dacc / l;
-    if (gq == 0) {
-      lse_s[pos] = lse;
-      dlt_s[pos] = delta;
-    }
+    const float lse = LSE ? lse_in : m + __log2f(l);  // relative to M_h
+    const float delta = LSE ? dlt_o : dacc / l;
 
     // loop B: dS, dQ^, bias / scale gradients
-    hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    float lk = 0.f, pp = 0.f, ps = 0.f;  // LSE: row sums of dS, P and P * sc2 cos
 #pragma unroll 1
-    for (int c = 0; c < K::NC; ++c) {
-      float ds[2][4];
+    for (int c = 0; c < (HVK_LARGE_PROBE == 5 ? 0 : K::NC); ++c) {
+      float ds[2][4], pl[2][4];
       int bidx[2][4];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -483,6 +498,12 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
           ds[t][r] = dsv;
           bidx[t][r] = qi.b - (ky * K::R + kx + r);
           if (kvalid) dscale += dsv * (s[r] - c4[r]);  // sc2 * cos (the mask only where p ~ 0)
+          if (LSE) {
+            pl[t][r] = p;
+            lk += dsv;
+            pp += p;
+            if (kvalid) ps = fmaf(p, s[r] - c4[r], ps);
+          }
         }
       }
       // CPB-table gradient: this wave's own bins (plain LDS read-add-write, no float atomics).
@@ -525,8 +546,33 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
                                   hvk_pack2(scale * ds[0][2], scale * ds[0][3]),
                                   hvk_pack2(scale * ds[1][0], scale * ds[1][1]),
                                   hvk_pack2(scale * ds[1][2], scale * ds[1][3]));
-      dq[0] = hvk_mfma16(tr_frag(img0, c, 0, li, gq), bf, dq[0]);
-      dq[1] = hvk_mfma16(tr_frag(img0, c, 1, li, gq), bf, dq[1]);
+      const uint4 kf0 = tr_frag(img0, c, 0, li, gq), kf1 = tr_frag(img0, c, 1, li, gq);
+      dq[0] = hvk_mfma16(kf0, bf, dq[0]);
+      dq[1] = hvk_mfma16(kf1, bf, dq[1]);
+      if (LSE) {  // sum_k P k^ of this query tile, for the dQ correction
+        const uint4 pf = make_uint4(hvk_pack2(pl[0][0], pl[0][1]), hvk_pack2(pl[0][2], pl[0][3]),
+                                    hvk_pack2(pl[1][0], pl[1][1]), hvk_pack2(pl[1][2], pl[1][3]));
+        pk[0] = hvk_mfma16(kf0, pf, pk[0]);
+        pk[1] = hvk_mfma16(kf1, pf, pk[1]);
+      }
+    }
+    float dlt = delta;
+    if (LSE) {
+      // dS = P (dP - delta_O) misses the exact P (dP - sum P dP / sum P) by P corr per row,
+      // corr = rowsum(dS) / rowsum(P): take it out of dQ (scale corr sum_k P k^) and of the
+      // logit-scale gradient, and hand phase 2 the exact delta
+      const float corr = hvk_group4_sum(lk) / hvk_group4_sum(pp);
+      const float psq = hvk_group4_sum(ps);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dq[dt][r] = fmaf(-scale * corr, pk[dt][r], dq[dt][r]);
+      if (gq == 0) dscale = fmaf(-corr, psq, dscale);
+      dlt = delta + corr;
+    }
+    if (gq == 0) {
+      lse_s[pos] = lse;
+      dlt_s[pos] = dlt;
     }
     normalize_bwd_store(qp, rnq, dq, a.dqkv + (size_t)qrow * C3 + h * 32, 1.f, gq, dqb);
   }
@@ -549,7 +595,7 @@ __global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(
   __syncthreads();
 
   // ---------------- phase 2: key tiles (key on the lane)
-  for (int kt = wave; kt < K::NT; kt += K::BWAVES) {
+  for (int kt = wave; kt < (HVK_LARGE_PROBE == 4 ? 0 : K::NT); kt += K::BWAVES) {
     const int pos = 16 * kt + li;
     const int krow = window_token_row(g, b, wh, ww, WIN, pos);
     const hvk_bf16* kp = a.qkv + (size_t)krow * C3 + h * 32 + C;
@@ -647,34 +693,47 @@ __global__ __launch_bounds__(256) void wmsa_finalize_large_kernel(BwdArgs a, flo
   finalize_scale_qb(a.dscale_acc, a.dqb_acc, dscale, dqb, h);
 }
 
-template <int WIN>
-int launch_fwd_large(const FwdArgs& a, hipStream_t st) {
+template <int WIN, bool LSE>
+int launch_fwd_large_(const FwdArgs& a, hipStream_t st) {
   using K = LCfg<WIN>;
   const size_t lds = 2 * (size_t)K::IMG + ((size_t)K::TABM + K::WAVES) * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_large_kernel<WIN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_large_kernel<WIN, LSE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const int padded = (a.g.n_windows + 7) / 8 * 8;
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, wmsa_fwd_large_kernel<WIN>, dim3(padded * a.g.nH), dim3(K::THREADS), lds, st, a);
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_large_kernel<WIN, LSE>), dim3(padded * a.g.nH),
+                   dim3(K::THREADS), lds, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd_large");
+  return HVK_OK;
+}
+template <int WIN>
+int launch_fwd_large(const FwdArgs& a, hipStream_t st) {
+  return a.lse ? launch_fwd_large_<WIN, true>(a, st) : launch_fwd_large_<WIN, false>(a, st);
+}
+
+template <int WIN, bool LSE>
+int launch_bwd_large_(const BwdArgs& a, hipStream_t st) {
+  using K = LCfg<WIN>;
+  const size_t lds = bwd_large_lds<WIN>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_large_kernel<WIN, LSE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int padded = (a.g.n_windows + 7) / 8 * 8;
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_large_kernel<WIN, LSE>), dim3(padded * a.g.nH),
+                   dim3(K::BTHREADS), lds, st, a);
   return HVK_OK;
 }
 
 template <int WIN>
 int launch_bwd_large(const BwdArgs& a, float* dtab, float* dscale, float* dqb, hipStream_t st) {
-  using K = LCfg<WIN>;
-  const size_t lds = bwd_large_lds<WIN>();
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_large_kernel<WIN>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
-  const int padded = (a.g.n_windows + 7) / 8 * 8;
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_large_kernel<WIN>, dim3(padded * a.g.nH), dim3(K::BTHREADS), lds, st, a);
+  if (a.lse) launch_bwd_large_<WIN, true>(a, st);
+  else launch_bwd_large_<WIN, false>(a, st);
   HVK_CHECK_LAUNCH("wmsa_bwd_large");
   hipLaunchKernelGGL(wmsa_finalize_large_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dtab, dscale, dqb);
   HVK_CHECK_LAUNCH("wmsa_finalize_large");

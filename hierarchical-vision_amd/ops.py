@@ -360,6 +360,9 @@ def _wmsa_workspace(device, nbytes):
 
 
 _WMSA_KL = os.environ.get("HVK_WMSA_BWD_KL", "0") == "1"  # 1: key-on-lane backward (probe)
+# windows 12 / 16 / 24: the forward keeps the row constants and the backward skips its
+# row-statistics pass (0: recompute them, A/B runs)
+_WMSA_LARGE_LSE = os.environ.get("HVK_WMSA_LARGE_LSE", "1") != "0"
 
 
 class WindowAttentionCore(torch.autograd.Function):
@@ -370,9 +373,9 @@ class WindowAttentionCore(torch.autograd.Function):
     swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h).  `q_bias` is taken only to
     route its gradient: d loss / d q_bias = column sums of dq, produced by the backward
     kernel (the qkv GEMM gets the bias detached, so no separate reduction runs).  For windows
-    <= 8 the forward also keeps each query's softmax row constant (4 B per token and head) and
-    the backward takes it with the output (kept anyway as proj's saved input) instead of
-    recomputing the softmax."""
+    12 / 16 / 24 (and <= 8 with HVK_WMSA_BWD_KL=1) the forward also keeps each query's softmax
+    row constant (4 B per token and head) and the backward takes it with the output (kept
+    anyway as proj's saved input) instead of recomputing the row statistics."""
 
     @staticmethod
     def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift):
@@ -384,8 +387,8 @@ class WindowAttentionCore(torch.autograd.Function):
         bias_table = _f32(bias_table)
         scale = _f32(scale)
         out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
-        lse = (torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32)
-               if _WMSA_KL and window <= 8 else None)
+        keep = (_WMSA_KL and window <= 8) or (_WMSA_LARGE_LSE and window > 8)
+        lse = torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32) if keep else None
         call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(lse), ptr(bias_table), ptr(scale), B, H, W, C,
              num_heads, window, shift, stream())
         if lse is not None:

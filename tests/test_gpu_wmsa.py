@@ -186,3 +186,32 @@ def test_wmsa_backward_paths_agree(monkeypatch, B, H, W, nh, win, shift):
     for name, a, b in zip(("dqkv", "dbias", "dscale", "dq_bias"), res[True], res[False]):
         rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
         assert rel < (3e-2 if name == "dscale" else 1e-2), (name, rel)
+
+
+
+@pytest.mark.parametrize("B,H,W,nh,win,shift", [(1, 24, 24, 2, 12, 6), (1, 48, 48, 2, 24, 12),
+                                                (1, 24, 24, 3, 24, 0), (1, 32, 32, 2, 16, 8)])
+@pytest.mark.parametrize("scale_kind", ["random", "anti100"])
+def test_wmsa_large_backward_paths_agree(monkeypatch, B, H, W, nh, win, shift, scale_kind):
+    """Large windows: the backward from the forward's row constants (delta from dO . O, then
+    corrected by loop B's own row sums) and the recomputing backward agree, including the
+    logit-scale gradient at scale 100 with anti-aligned q / k."""
+    import hvamd.ops as ops
+    if scale_kind == "random":
+        qkv, tab, scale = _inputs(B, H, W, nh, win, 4)
+    else:
+        qkv, tab, scale = _anti_aligned(B, H, W, nh, win, 5, shared=False)
+    gout = torch.from_numpy(np.random.default_rng(6).standard_normal((B, H * W, 32 * nh)).astype(np.float32))
+    res = {}
+    for keep in (True, False):
+        monkeypatch.setattr(ops, "_WMSA_LARGE_LSE", keep)
+        q = qkv.cuda().bfloat16().requires_grad_(True)
+        t = tab.cuda().requires_grad_(True)
+        s = scale.cuda().requires_grad_(True)
+        qb = torch.zeros(32 * nh, device="cuda", requires_grad=True)
+        ops.window_attention_core(q, t, s, H, W, nh, win, shift, q_bias=qb).backward(gout.cuda().bfloat16())
+        res[keep] = [x.grad.float().cpu() for x in (q, t, s, qb)]
+    for name, a, b in zip(("dqkv", "dbias", "dscale", "dq_bias"), res[True], res[False]):
+        assert torch.isfinite(a).all(), name
+        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+        assert rel < (3e-2 if name in ("dscale", "dbias") else 1e-2), (name, rel)
