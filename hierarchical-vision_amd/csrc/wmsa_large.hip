@@ -24,6 +24,9 @@
 #ifndef HVK_LARGE_PROBE
 #define HVK_LARGE_PROBE 0
 #endif
+#ifndef HVK_LARGE_FWAVES24  // forward waves per workgroup at w24 (9 / 12 / 16: 19.3 / 18.3 / 16.9 ms per SwinV2-B 384 step)
+#define HVK_LARGE_FWAVES24 16
+#endif
 #ifndef HVK_LARGE_BINS
 #define HVK_LARGE_BINS 1
 #endif
@@ -39,7 +42,7 @@ struct LCfg {
   static constexpr int ROWS = 32 * NC;         // padded rows of an LDS image
   static constexpr int R = 2 * WIN - 1;
   static constexpr int RR = R * R;             // CPB table entries per head
-  static constexpr int WAVES = WIN == 16 ? 8 : 9;
+  static constexpr int WAVES = WIN == 16 ? 8 : (WIN == 24 ? HVK_LARGE_FWAVES24 : 9);
   static constexpr int THREADS = 64 * WAVES;
   static constexpr int QB = (NT % (2 * WAVES) == 0) ? 2 : 1;  // query tiles per forward pass
   static constexpr int IMG = ROWS * 64;        // bytes per image
