@@ -54,16 +54,18 @@ int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double
  * scale: f32 [num_heads] = exp(clamp(logit_scale, max=ln 100)) (swinv2.py:230).
  * window/shift are the clamped values of swinv2.py:328-331.  head_dim must be 32; window
  * in {4, 6, 7, 8} (one wave per (window, head)) or {12, 16, 24} (one workgroup each).
- * lse: NULL, or f32 [B*H*W, num_heads] (windows <= 8; ignored for 12/16/24): per query and
- * head, L2 = log2 sum_k exp2(log2e * logit), the row constant of the softmax that the
- * key-on-lane backward consumes (P = exp2(log2e * logit - L2)). */
+ * lse: NULL, or f32 [B*H*W, num_heads]: per query and head, L2 = log2 sum_k exp2(log2e *
+ * logit), the row constant of the softmax that the backward can consume (P = exp2(log2e *
+ * logit - L2)). */
 int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
                  int B, int H, int W, int C, int num_heads, int window, int shift,
                  void* stream);
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
-/* dout: bf16 [B*H*W, C] (grad of `out`); out, lse: the forward's output and row constants
- * (windows <= 8: the key-on-lane kernel, delta = rowsum(dout o out) instead of a recomputed
- * softmax), or both NULL (every window: the softmax is recomputed from q, k);
+/* dout: bf16 [B*H*W, C] (grad of `out`); out, lse: the forward's output and row constants,
+ * or both NULL (every window: the softmax row statistics are recomputed from q, k).  Given
+ * them, windows <= 8 run the key-on-lane kernel (delta = rowsum(dout o out)), windows
+ * 12/16/24 skip the row-statistics pass (delta from dout o out, corrected by the exact dS
+ * and P row sums for dq, dk, dv and dscale);
  * dqkv: bf16 [B*H*W, 3C] (fully overwritten);
  * dq_bias: f32 [C] (overwritten: column sums of the q part of dqkv = d loss / d q_bias,
  * replacing the qkv bias-gradient reduction) or NULL; dbias_table: f32 [num_heads,
