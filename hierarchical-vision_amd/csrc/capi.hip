@@ -20,7 +20,7 @@ int hvk_set_error(int code, const char* fmt, ...) {
 
 const char* hvk_last_error_string(void) { return g_hvk_err; }
 
-int hvk_abi_version(void) { return 4; }
+int hvk_abi_version(void) { return 5; }
 
 // ---- kernel timer ------------------------------------------------------------------
 namespace {
@@ -32,10 +32,11 @@ struct TimerRec {
 std::vector<TimerRec> g_timer;  // event pool (created once, reused)
 size_t g_timer_used = 0;
 bool g_timer_on = false;
+int g_timer_kinds = 0xF;  // bit k: time launches of kind k
 }  // namespace
 
 void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop) {
-  if (!g_timer_on || g_timer_used >= g_timer.size()) {
+  if (!g_timer_on || !((g_timer_kinds >> kind) & 1) || g_timer_used >= g_timer.size()) {
     *start = *stop = nullptr;
     return;
   }
@@ -55,6 +56,11 @@ int hvk_kernel_timer_enable(int max_launches) {
       return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_enable: hipEventCreate failed");
     g_timer.push_back(r);
   }
+  return HVK_OK;
+}
+
+int hvk_kernel_timer_kinds(int mask) {
+  g_timer_kinds = mask;
   return HVK_OK;
 }
 

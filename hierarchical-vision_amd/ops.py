@@ -14,9 +14,13 @@ from . import _lib
 from ._lib import call, ptr, stream
 
 
-def kernel_timer_start(max_launches=32768):
-    """Time the next W-MSA and GEMM launches inside libhvk (dispatch-packet events,
-    include/hvk.h)."""
+TIMER_WMSA, TIMER_GEMM, TIMER_ALL = 0x3, 0xC, 0xF  # kind masks (include/hvk.h)
+
+
+def kernel_timer_start(max_launches=32768, kinds=TIMER_ALL):
+    """Time the next W-MSA and / or GEMM launches inside libhvk (dispatch-packet events,
+    include/hvk.h); `kinds` is a bit mask of timer kinds."""
+    call("hvk_kernel_timer_kinds", int(kinds))
     call("hvk_kernel_timer_enable", int(max_launches))
 
 

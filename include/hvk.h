@@ -40,6 +40,9 @@ const char* hvk_last_error_string(void);
  * algorithmic work of those launches (GEMMs: 2 M N K flops each; W-MSA: 0). */
 int hvk_kernel_timer_enable(int max_launches);
 int hvk_kernel_timer_read(int kind, double* total_ms, int* launches);
+/* which kinds the timer records (bit k = kind k; default 0xF, all): bench.py times only the
+ * W-MSA launches inside its timed steps and the GEMMs in extra steps after them */
+int hvk_kernel_timer_kinds(int mask);
 int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double* work);
 
 /* ---- Shifted-window cosine attention core ------------------------------------------
