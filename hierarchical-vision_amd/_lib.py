@@ -40,6 +40,7 @@ SIGNATURES = {
     "hvk_gemm_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_gelu_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_gemm_set_pp": (_i, [_i]),
     "hvk_weight_grad_supported": (_i, [_i, _i, _i]),
     "hvk_cast_weights": (_i, [_i, _p, _p, _p, _p, _p, _p]),
     "hvk_block_bias_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p,
@@ -95,7 +96,12 @@ def load():
                 "g.build()'` (or `make -C hierarchical-vision_amd/csrc`).  There is no fallback.")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            # an older A/B build (HVK_LIB_PATH) may predate an entry point; the shipped one may not
+            fn = getattr(lib, name, None)
+            if fn is None:
+                if os.environ.get("HVK_LIB_PATH"):
+                    continue
+                raise RuntimeError(f"{LIB_PATH} does not export {name} (stale build?)")
             fn.restype = res
             fn.argtypes = args
         _lib = lib

@@ -63,6 +63,89 @@ __device__ __forceinline__ uint4 tie(hvk_u32x4 v) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
+// Epilogue shared by both tiled kernels: acc[t][b] of a lane (li, gq) holds W-tile t x token
+// tile b of a wave whose tokens start at row0 and columns at col0; tiles 2j, 2j+1 give the 8
+// consecutive columns col0 + 32j + 8gq .. +7 of token row0 + 16b + li (perm_row).  Bias / h
+// loads first, every output packed, then all 16-B stores back to back: a register still read
+// by an outstanding store cannot be rewritten before vmcnt says so, and a load waited for
+// between stores would wait for every store before it (vmcnt counts in order).
+template <int EPI, int NT, int MT>
+__device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
+                                              hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
+                                              int N, int row0, int col0) {
+  const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+  float bv[NT / 2][8];
+  if (EPI != 2 && bias) {
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + col0 + 32 * j + 8 * gq);
+      const float4 b1 = *reinterpret_cast<const float4*>(bias + col0 + 32 * j + 8 * gq + 4);
+      bv[j][0] = b0.x; bv[j][1] = b0.y; bv[j][2] = b0.z; bv[j][3] = b0.w;
+      bv[j][4] = b1.x; bv[j][5] = b1.y; bv[j][6] = b1.z; bv[j][7] = b1.w;
+    }
+  }
+  uint4 hp[EPI == 2 ? MT : 1][NT / 2];
+  if (EPI == 2) {  // gh = (gy w) * GELU'(h): h (Y2) read in the output layout
+#pragma unroll
+    for (int b = 0; b < MT; ++b) {
+      int row = row0 + 16 * b + li;
+      if (row >= M) row = M - 1;
+#pragma unroll
+      for (int j = 0; j < NT / 2; ++j)
+        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq);
+    }
+  }
+  hvk_u32x4 pk[MT][NT / 2], pg[EPI == 1 ? MT : 1][NT / 2];
+#pragma unroll
+  for (int b = 0; b < MT; ++b)
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[2 * j][b][r];
+        v[4 + r] = acc[2 * j + 1][b][r];
+      }
+      if (EPI != 2 && bias) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bv[j][e];
+      }
+      if (EPI == 2) {
+        float hf[8];
+        hvk_unpack8(hp[b][j], hf);
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hf[e], hf[e + 1]});
+          v[e] *= d.x;
+          v[e + 1] *= d.y;
+        }
+      }
+      const uint4 hv = hvk_pack8(v);
+      pk[b][j] = __builtin_bit_cast(hvk_u32x4, hv);
+      if (EPI == 1) pg[b][j] = __builtin_bit_cast(hvk_u32x4, hvk_gelu8_bf16(hv));  // GELU of the rounded h
+    }
+  // pin the packing here (else hipcc sinks it into each row's store branch and reuses the
+  // registers of the previous row's stores)
+#pragma unroll
+  for (int b = 0; b < MT; ++b)
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      asm volatile("" : "+v"(pk[b][j]));
+      if (EPI == 1) asm volatile("" : "+v"(pg[b][j]));
+    }
+#pragma unroll
+  for (int b = 0; b < MT; ++b) {
+    const int row = row0 + 16 * b + li;
+    if (row >= M) continue;
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      const size_t o = (size_t)row * N + col0 + 32 * j + 8 * gq;
+      *reinterpret_cast<hvk_u32x4*>(Y + o) = pk[b][j];
+      if (EPI == 1) *reinterpret_cast<hvk_u32x4*>(Y2 + o) = pg[b][j];
+    }
+  }
+}
+
 template <int EPI, bool PIPE, int TN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
                                                         const hvk_bf16* __restrict__ Wt,
@@ -201,66 +284,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  // EPI 2: the 8 h vectors of this lane, loaded as one batch before the epilogue math
-  uint4 hp[EPI == 2 ? 4 : 1][TN / 2];
-  if (EPI == 2) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      int row = m0 + 64 * wm + 16 * b + li;
-      if (row >= M) row = M - 1;
-#pragma unroll
-      for (int j = 0; j < TN / 2; ++j)
-        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + n0 + 16 * TN * wn + 32 * j + 8 * g);
-    }
-  }
-  // epilogue: lane (li, g) holds, for m-tile b and n-tile pair (2j, 2j+1), row
-  // m0 + 64wm + 16b + li and columns n0 + 16 TN wn + 32j + 8g .. +7
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const int row = m0 + 64 * wm + 16 * b + li;
-    if (row >= M) continue;
-#pragma unroll
-    for (int j = 0; j < TN / 2; ++j) {
-      const int col = n0 + 16 * TN * wn + 32 * j + 8 * g;
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = acc[2 * j][b][r];
-        v[4 + r] = acc[2 * j + 1][b][r];
-      }
-      if (EPI != 2 && bias) {
-        const float4 b0 = *reinterpret_cast<const float4*>(bias + col);
-        const float4 b1 = *reinterpret_cast<const float4*>(bias + col + 4);
-        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-      }
-      if (EPI == 2) {  // gh = (gy w) * GELU'(h): h (Y2) read in the output layout
-        float hf[8];
-        hvk_unpack8(hp[b][j], hf);
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hf[e], hf[e + 1]});
-          v[e] *= d.x;
-          v[e + 1] *= d.y;
-        }
-        *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hvk_pack8(v);
-        continue;
-      }
-      const uint4 hv = hvk_pack8(v);
-      *reinterpret_cast<uint4*>(Y + (size_t)row * N + col) = hv;
-      if (EPI == 1) {
-        float u[8];
-        hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-            const hvk_gelu::f32x2 y = hvk_gelu::gelu2(hvk_gelu::f32x2{u[e], u[e + 1]});
-            u[e] = y.x;
-            u[e + 1] = y.y;
-          }
-        *reinterpret_cast<uint4*>(Y2 + (size_t)row * N + col) = hvk_pack8(u);
-      }
-    }
-  }
+  tile_epilogue<EPI, TN, 4>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
@@ -271,6 +295,229 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     q[5] = __builtin_amdgcn_s_getreg(63508);  // XCC_ID
   }
 #endif
+}
+
+// ---- ping-pong tiled GEMM (one 512-thread workgroup per CU) ---------------------------------
+// The kernel above runs two barriers per 64-deep k-step with all of a workgroup's waves in the
+// same state: they wait for the stage together, read fragments together, then all issue MFMAs,
+// so the L2->LDS stream, the LDS reads and the MFMAs take turns (the k-step measured 0.77 us
+// against 0.43 us of MFMA work).  Here 8 waves form two groups of 4 that run the SAME phase
+// sequence one barrier apart: a phase is [fragment reads + LDS-DMA issue] barrier [16 MFMAs]
+// barrier, so while one group's MFMAs run on a SIMD the other group's wave on that SIMD reads
+// and issues DMA (s_setprio 1 over each MFMA cluster).  Group g owns tokens g*16*WTM .. +16*WTM
+// of the tile, wave c of a group owns columns c*16*WTN .. +16*WTN; a k-step is 4 phases, one
+// per quadrant (token half x column half) of the wave's tile, visited (0,0) (0,1) (1,1) (1,0) so
+// that every fragment is read once per k-step.  Tiles: 256 x 256 (WTM 8, WTN 4) and 128 x 384
+// (WTM 4, WTN 6), both 64 KB per k-step stage, two stages (128 KB).  The next k-step's stage is
+// DMA'd during phases 1-3 of this one and waited (own vmcnt(0)) in phase 4, one barrier before
+// the other group first reads it; a stage is overwritten only after phase 3 of both groups,
+// which hold every fragment of it in registers by then (their reads are waited before their
+// MFMAs, i.e. before the next barrier).
+template <int EPI, int WTM, int WTN>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const hvk_bf16* __restrict__ X,
+                                                       const hvk_bf16* __restrict__ Wt,
+                                                       const float* __restrict__ bias,
+                                                       hvk_bf16* __restrict__ Y,
+                                                       hvk_bf16* __restrict__ Y2, int M, int N, int K,
+                                                       int mtiles) {
+  constexpr int BMP = 32 * WTM, BNP = 64 * WTN;  // tile tokens x columns
+  constexpr int STAGE = (BMP + BNP) * 128;       // bytes per 64-deep k-step
+  constexpr int NI = (BMP + BNP) / 64;           // DMA wave-instructions per wave and stage (8)
+  static_assert(NI == 8, "stage split assumes 8 DMA instructions per wave");
+  constexpr int HM = WTM / 2, HN = WTN / 2;      // quadrant tiles
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntiles = N / BNP;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+  const int nt = loc % ntiles, mt = (loc / ntiles) * 8 + xcd;
+  if (mt >= mtiles) return;
+  const int m0 = mt * BMP, n0 = nt * BNP;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int grp = wave >> 2, wc = wave & 3;
+  const int li = lane & 15, gq = lane >> 4;
+  const int KT = K / BK;
+
+  // A stage is refilled per REGION, two phases after the region's last fragment read (the
+  // other group reads it one barrier later): R1 = the first token half of each group's X rows
+  // + the first column half of each wave's W rows (read in phase 0), R2 = the second column
+  // halves (phase 1), R3 = the second token halves (phase 2).  K-step kt+2's R1 / R2 are
+  // issued in phases 2 / 3 of kt and its R3 in phase 0 of kt+1, so each region has ~1.5
+  // k-steps to land.  A region is a list of 8-row blocks (one 1-KB DMA wave-instruction each),
+  // block i of a list loaded by wave i % 8: R1 2WTM + 4WTN = 32 blocks (4 per wave), R2 4WTN,
+  // R3 2WTM (8 per wave in all).  Lane L of a block -> image row 8b + L/8, LDS chunk L%8 <-
+  // global chunk (L%8) ^ (L/8).
+  constexpr int N2 = WTN / 2, N3 = WTM / 4;  // R2 / R3 instructions per wave (R1: 4)
+  static_assert(4 * WTN == 8 * N2 && 2 * WTM == 8 * N3 && 2 * WTM + 4 * WTN == 32, "region split");
+  const int lr = lane >> 3, lc = lane & 7;
+  uint32_t src[NI], dst[NI];
+  bool isx[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    int blk;  // X block (< 2 * 2WTM... image rows / 8) or W block (+ BMP / 8)
+    if (i < 4) {  // R1: X first halves (group 0, 1), then W first halves (waves 0..3)
+      const int q = wave + 8 * i;
+      if (q < 2 * WTM) blk = (q / WTM) * 2 * WTM + q % WTM;
+      else { const int r = q - 2 * WTM; blk = BMP / 8 + (r / WTN) * 2 * WTN + r % WTN; }
+    } else if (i < 4 + N2) {  // R2: W second halves
+      const int r = wave + 8 * (i - 4);
+      blk = BMP / 8 + (r / WTN) * 2 * WTN + WTN + r % WTN;
+    } else {  // R3: X second halves
+      const int q = wave + 8 * (i - 4 - N2);
+      blk = (q / WTM) * 2 * WTM + WTM + q % WTM;
+    }
+    isx[i] = blk < BMP / 8;
+    dst[i] = blk * 1024;
+    const int row = 8 * blk + lr;
+    if (isx[i]) {
+      int xr = m0 + row;
+      if (xr >= M) xr = M - 1;  // rows past M: any valid row (never stored)
+      src[i] = (uint32_t)xr * K + 8 * (lc ^ lr);
+    } else {
+      src[i] = (uint32_t)(n0 + perm_row(row - BMP)) * K + 8 * (lc ^ lr);
+    }
+  }
+  auto dma = [&](int i, int kt) {
+    const hvk_bf16* s = (isx[i] ? X : Wt) + src[i] + kt * BK;
+    __builtin_amdgcn_global_load_lds((gbl_vptr_t)s, (lds_vptr_t)(smem + (kt & 1) * STAGE + dst[i]), 16, 0, 0);
+  };
+  auto dma_region = [&](int r, int kt) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if ((r == 1 && i < 4) || (r == 2 && i >= 4 && i < 4 + N2) || (r == 3 && i >= 4 + N2)) dma(i, kt);
+  };
+  // wait for the region of k-step tt: 8 DMAs of this wave are younger iff k-step tt+1 exists
+  auto wait_region = [&](int tt) {
+    if (tt + 1 < KT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  hvk_f32x4 acc[WTN][WTM];
+#pragma unroll
+  for (int a = 0; a < WTN; ++a)
+#pragma unroll
+    for (int b = 0; b < WTM; ++b) acc[a][b] = hvk_f32x4{0, 0, 0, 0};
+
+  // prologue: k-steps 0 and 1 (regions in order R1 R2 R3), wait for k-step 0
+#pragma unroll
+  for (int r = 1; r <= 3; ++r) dma_region(r, 0);
+  if (KT > 1) {
+#pragma unroll
+    for (int r = 1; r <= 3; ++r) dma_region(r, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  hvk_u32x4 xf[HM][2], wf[WTN][2];
+  const uint32_t xrow = lds_u32(smem) + (16 * WTM * grp + li) * 128;
+  const uint32_t wrow = lds_u32(smem) + (BMP + 16 * WTN * wc + li) * 128;
+  const uint32_t sw0 = ((gq) ^ (li & 7)) << 4, sw1 = ((4 + gq) ^ (li & 7)) << 4;
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const uint32_t sb = (kt & 1) * STAGE;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int hm = (p == 0 || p == 1) ? 0 : 1;  // quadrants (0,0) (0,1) (1,1) (1,0)
+      const int hn = (p == 0 || p == 3) ? 0 : 1;
+      // ---- memory part: this quadrant's new fragments, then the region waits / refills
+      if (p == 0 || p == 2) {
+#pragma unroll
+        for (int t = 0; t < HM; ++t) {
+          const uint32_t a = xrow + sb + (HM * hm + t) * 2048;
+          asm volatile("ds_read_b128 %0, %1" : "=v"(xf[t][0]) : "v"(a + sw0));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(xf[t][1]) : "v"(a + sw1));
+        }
+      }
+      if (p == 0 || p == 1) {
+#pragma unroll
+        for (int t = 0; t < HN; ++t) {
+          const uint32_t a = wrow + sb + (HN * hn + t) * 2048;
+          asm volatile("ds_read_b128 %0, %1" : "=v"(wf[HN * hn + t][0]) : "v"(a + sw0));
+          asm volatile("ds_read_b128 %0, %1" : "=v"(wf[HN * hn + t][1]) : "v"(a + sw1));
+        }
+      }
+      if (p == 0) {  // R2(kt) is read next phase; R3(kt+1) into the region phase 2 of kt-1 freed
+        wait_region(kt);
+        if (kt >= 1 && kt + 1 < KT) dma_region(3, kt + 1);
+      } else if (p == 1) {
+        wait_region(kt);  // R3(kt)
+      } else if (p == 2) {
+        if (kt + 2 < KT) dma_region(1, kt + 2);
+      } else {
+        wait_region(kt + 1);  // R1(kt+1)
+        if (kt + 2 < KT) dma_region(2, kt + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- MFMA part
+      uint4 xa[HM][2], wa[HN][2];
+#pragma unroll
+      for (int t = 0; t < HM; ++t) { xa[t][0] = tie(xf[t][0]); xa[t][1] = tie(xf[t][1]); }
+#pragma unroll
+      for (int t = 0; t < HN; ++t) { wa[t][0] = tie(wf[HN * hn + t][0]); wa[t][1] = tie(wf[HN * hn + t][1]); }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int a = 0; a < HN; ++a)
+#pragma unroll
+          for (int b = 0; b < HM; ++b)
+            acc[HN * hn + a][HM * hm + b] = hvk_mfma16(wa[a][ks], xa[b][ks], acc[HN * hn + a][HM * hm + b]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // balance group 1's extra barrier
+
+  tile_epilogue<EPI, WTN, WTM>(acc, bias, Y, Y2, M, N, m0 + 16 * WTM * grp, n0 + 16 * WTN * wc);
+}
+
+template <int EPI, int WTM, int WTN>
+int launch_pp_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
+               int M, int N, int K, hipStream_t st) {
+  constexpr int BMP = 32 * WTM, BNP = 64 * WTN, LDS = 2 * (BMP + BNP) * 128;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, WTM, WTN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int mtiles = (M + BMP - 1) / BMP;
+  const dim3 grid((mtiles + 7) / 8 * 8 * (N / BNP));
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_pp_kernel<EPI, WTM, WTN>), grid, dim3(512),
+                     LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles);
+  HVK_CHECK_LAUNCH("hvk_gemm_tile(pp)");
+  return HVK_OK;
+}
+
+// ping-pong tile choice: 0 (default) off, 1 wherever a ping-pong tile divides N, 2 only
+// 256 x 256, 3 only 128 x 384; initial value from HVK_GEMM_PP, changed by hvk_gemm_set_pp
+// (A/B runs and the tests that pin both kernels to the same bits).  Off by default: measured
+// 3-25 % slower than the 128-row tiles on every SwinV2 stage 1-3 shape (tools/bench_pp.py)
+static int g_pp_mode = -1;
+static int gemm_pp_mode() {
+  if (g_pp_mode < 0) {
+    const char* e = getenv("HVK_GEMM_PP");
+    g_pp_mode = e ? atoi(e) : 0;
+  }
+  return g_pp_mode;
+}
+
+template <int EPI>
+int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2, int M,
+              int N, int K, hipStream_t st) {
+  const int mode = gemm_pp_mode();
+  // element offsets are 32-bit in the kernel
+  if (mode == 0 || (size_t)M * K >= (1u << 31) || (size_t)N * K >= (1u << 31)) return -1;
+  if (N % 256 == 0 && mode != 3) return launch_pp_<EPI, 8, 4>(X, W, bias, Y, Y2, M, N, K, st);
+  if (N % 384 == 0 && mode != 2) return launch_pp_<EPI, 4, 6>(X, W, bias, Y, Y2, M, N, K, st);
+  return -1;
 }
 
 static bool tile_pipe() {
@@ -311,6 +558,10 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
     const char* e = getenv("HVK_TILE_WIDE");
     return e ? atoi(e) : -1;
   }();
+  {
+    const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
+    if (r >= 0) return r;
+  }
   const bool wide = N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536));
   if (N % TileCfg<4>::BN == 0 && !wide)
     return tile_pipe() ? launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st)
@@ -329,6 +580,13 @@ int hvk_gemm_probe_read(void* dst, int nblocks) {
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
+
+int hvk_gemm_set_pp(int mode) {
+  if (mode < 0 || mode > 3) return hvk_set_error(HVK_EINVAL, "hvk_gemm_set_pp: mode %d not in 0..3", mode);
+  const int prev = gemm_pp_mode();
+  g_pp_mode = mode;
+  return prev;
+}
 
 int hvk_gemm_supported(int M, int K, int N) {
   return M > 0 && K >= BK && K % BK == 0 && (N % TileCfg<4>::BN == 0 || N % TileCfg<6>::BN == 0) &&

@@ -128,6 +128,12 @@ int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, 
  * w [N, K] (= fc2.weight^T), h [M, N] the saved pre-activation. */
 int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, int M, int K, int N,
                       void* stream);
+/* Tile kernel selection for the three entry points above: 0 (default) = the 128 x 128 /
+ * 128 x 192 two-workgroups-per-CU kernel only, 1 = the ping-pong 256 x 256 / 128 x 384 kernel
+ * (one 8-wave workgroup per CU) wherever its tile divides N, 2 / 3 = only its 256 x 256 /
+ * 128 x 384 tile.  Both kernels accumulate in the same order, so their results are
+ * bit-identical.  Returns the previous mode (initially $HVK_GEMM_PP, else 0). */
+int hvk_gemm_set_pp(int mode);
 
 /* ---- Weight-gradient GEMM (the backward of every SwinV2 Linear) ----------------------
  * dw[N, K] = g[M, N]^T x[M, K] in f32 and, when db is not NULL, db[N] = sum_m g[m, n]

@@ -350,3 +350,50 @@ def test_attn_biases_match_torch(C):
     assert torch.equal(pb.grad, g)
     assert torch.allclose(w.grad, torch.outer(g, vb.detach()), rtol=1e-6, atol=1e-6)
     assert qb.grad is None
+
+
+@pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (12544, 768, 768), (777, 1536, 2304),
+                                   (300, 192, 384), (1000, 1152, 384), (3000, 64, 256)])
+@pytest.mark.parametrize("epi", ["plain", "bias", "gelu_fwd", "gelu_bwd"])
+def test_gemm_pingpong_bit_identical_to_two_wg_kernel(M, K, N, epi):
+    """The ping-pong kernel (256 x 256 / 128 x 384 tiles, hvk_gemm_set_pp) accumulates in the
+    same k order as the 128-row tile kernel, so every epilogue form must agree bit for bit;
+    ragged M and single-k-step K included."""
+    from hvamd import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + K + N)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    outs = []
+    prev = lib.hvk_gemm_set_pp(0)
+    try:
+        for mode in (0, 1):  # two-workgroup tiles, then ping-pong wherever it divides N
+            lib.hvk_gemm_set_pp(mode)
+            y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+            y2 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+            if epi in ("plain", "bias"):
+                _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b) if epi == "bias" else None,
+                          _lib.ptr(y), M, K, N, _lib.stream())
+            elif epi == "gelu_fwd":
+                _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2),
+                          M, K, N, _lib.stream())
+            else:
+                _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(h), _lib.ptr(y), M, K, N,
+                          _lib.stream())
+            torch.cuda.synchronize()
+            outs.append((y, y2))
+    finally:
+        lib.hvk_gemm_set_pp(prev)
+    (y0, y20), (y1, y21) = outs
+    assert not torch.isnan(y1.float()).any()
+    assert torch.equal(y0.view(torch.int16), y1.view(torch.int16))
+    if epi == "gelu_fwd":
+        assert torch.equal(y20.view(torch.int16), y21.view(torch.int16))
+    ref = x.float() @ w.float().t() + (b if epi in ("bias", "gelu_fwd") else 0)
+    if epi == "gelu_bwd":
+        hf = h.float().requires_grad_(True)
+        torch.nn.functional.gelu(hf).backward(ref)
+        ref = hf.grad
+    assert ((y1.float() - ref).norm() / ref.norm()).item() < 1e-2
