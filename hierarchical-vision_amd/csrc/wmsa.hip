@@ -32,6 +32,9 @@ namespace {
 using namespace hvk_wmsa;
 
 constexpr int kWaves = 4;
+#ifndef HVK_BWD_PF  // 1: next window's inputs loaded under phase B (see wmsa_bwd_kernel)
+#define HVK_BWD_PF 1
+#endif
 constexpr int kThreads = 64 * kWaves;
 
 
@@ -315,26 +318,39 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
   float dscale = 0.f;
   float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // this lane's column sums of dq
 
-  for (int w = w0 + wave; w < w1; w += kWaves) {
+  // q, k, v, dO of a window into registers.  HVK_BWD_PF: the next window's loads are issued
+  // right after phase A, into the registers phase A was the last to read (phase B works from
+  // the LDS images), so their latency hides under phase B instead of stalling the next window
+  int nrow[K::NT];
+  uint4 qf[K::NT], kf[K::NT], vf[K::NT], df[K::NT];
+  auto load_window = [&](int w) {
     const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
-    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
-    int row[K::NT];
-    uint4 qf[K::NT], kf[K::NT], vf[K::NT], df[K::NT];
-    float rnq[K::NT], rnk[K::NT];
 #pragma unroll
     for (int i = 0; i < K::NT; ++i) {
       const int t = 16 * i + li;
-      row[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
+      nrow[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
       if (t < K::N) {
-        const hvk_bf16* p = a.qkv + (size_t)row[i] * C3 + h * 32 + 8 * gq;
+        const hvk_bf16* p = a.qkv + (size_t)nrow[i] * C3 + h * 32 + 8 * gq;
         qf[i] = hvk_ld16(p);
         kf[i] = hvk_ld16(p + C);
         vf[i] = hvk_ld16(p + 2 * C);
-        df[i] = hvk_ld16(a.dout + (size_t)row[i] * C + h * 32 + 8 * gq);
+        df[i] = hvk_ld16(a.dout + (size_t)nrow[i] * C + h * 32 + 8 * gq);
       } else {
         qf[i] = kf[i] = vf[i] = df[i] = make_uint4(0, 0, 0, 0);
       }
     }
+  };
+  if (HVK_BWD_PF && w0 + wave < w1) load_window(w0 + wave);
+
+  for (int w = w0 + wave; w < w1; w += kWaves) {
+    const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    (void)b;
+    if (!HVK_BWD_PF) load_window(w);
+    int row[K::NT];
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) row[i] = nrow[i];
+    float rnq[K::NT], rnk[K::NT];
 #pragma unroll
     for (int i = 0; i < K::NT; ++i) {
       qf[i] = l2_normalize(qf[i], rnq[i]);
@@ -468,6 +484,7 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       }
     }
     asm volatile("" ::: "memory");  // same-wave LDS ops complete in order: compiler fence only
+    if (HVK_BWD_PF && w + kWaves < w1) load_window(w + kWaves);
 
     // ---------------- phase B: one key tile at a time, key on the lane
     // query chunk c, slot (g, j): q(g, j) = 32c + (j < 4 ? 4g + j : 16 + 4g + j - 4)
