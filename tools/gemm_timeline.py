@@ -1,6 +1,6 @@
 """Per-workgroup phase timeline of the tiled GEMM from the HVK_GEMM_PROBE=4 build
 (tools/probe/libhvk_gemm4.so): prologue (first tile landed), k-loop, epilogue (stores drained).
-    python tools/gemm_timeline.py M K N     (make -C tools/probe libhvk_gemm4.so first)"""
+    python tools/gemm_timeline.py M K N [gelu|gelu_bwd]   (make -C tools/probe libhvk_gemm4.so first)"""
 import ctypes
 import os
 import sys
@@ -13,16 +13,27 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     M, K, N = (int(a) for a in sys.argv[1:4])
+    epi = sys.argv[4] if len(sys.argv) > 4 else "plain"
     from hvamd import _lib
-    _lib.LIB_PATH = os.path.abspath("tools/probe/libhvk_gemm4.so")
+    _lib.LIB_PATH = os.path.abspath(os.environ.get("HVK_TL_LIB", "tools/probe/libhvk_gemm4.so"))
     lib = _lib.load()
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16()
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    y2 = torch.randn(M, N, device="cuda").bfloat16()
+    b = torch.randn(N, device="cuda")
     for _ in range(5):
-        _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), None, _lib.ptr(y), M, K, N, _lib.stream())
+        if epi == "gelu":
+            _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2), M, K,
+                      N, _lib.stream())
+        elif epi == "gelu_bwd":
+            _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y2), _lib.ptr(y), M, K, N,
+                      _lib.stream())
+        else:
+            _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), None, _lib.ptr(y), M, K, N, _lib.stream())
     torch.cuda.synchronize()
-    BM, BN = 128, 128
+    # tile width as launch_tile picks it (HVK_TILE_WIDE unset)
+    BM, BN = 128, (192 if N % 192 == 0 and (N > 384 or K >= 1536) else 128)
     mt = (M + BM - 1) // BM
     nb = (mt + 7) // 8 * 8 * (N // BN)
     buf = np.zeros(nb * 6, dtype=np.uint64)
