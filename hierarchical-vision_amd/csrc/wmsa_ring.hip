@@ -27,6 +27,9 @@
 #ifndef HVK_RING_PROBE
 #define HVK_RING_PROBE 0
 #endif
+#ifndef HVK_RING_AUX  // slab DMA cache policy (A/B builds): 2 nontemporal, 1 only for whole-row groups, 0 never
+#define HVK_RING_AUX 2
+#endif
 #ifndef HVK_RING_ROWMAX_CHECK  // 0: A/B probe builds without the underflow check (not exact)
 #define HVK_RING_ROWMAX_CHECK 1
 #endif
@@ -92,8 +95,14 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
         unsigned off = __umul24(pre[k % K::KP], 1u) + U;  // v_mad_u32_u24: low 24 bits of pre
         if (lx < WIN)  // last window column: per-lane wrap of the token column
           off -= ((int)(pre[k % K::KP] >> 24) >= lx) ? WRB : 0u;
-        __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0,
-                                         2 /* nontemporal: every byte is read once */);
+        // nontemporal: every byte is read once, and the hint keeps qkv from evicting what the
+        // next kernels read (this kernel's output feeds the proj GEMM).  HVK_RING_AUX = 1 drops
+        // it where several head groups share a token row: this kernel is then 2-6 % faster at
+        // stages 2-3 (tools/gpu_fwdaux.sh) but the step 0.4 % slower (interleaved A/B), so 2
+        if (HVK_RING_AUX == 2 || (HVK_RING_AUX == 1 && ng == 1))
+          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 2);
+        else
+          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 0);
       }
     }
   };
