@@ -104,7 +104,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     const bool ok = t < tiles && row < M;
 #pragma unroll
     for (int j = 0; j < G::NT / 2; ++j)
-      hf[j] = ok ? hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j) : make_uint4(0, 0, 0, 0);
+      hf[j] = ok ? ((HVK_NT_SAVED & 8) ? hvk_ld16_nt(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j)
+                                       : hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j))
+                 : make_uint4(0, 0, 0, 0);
   };
   uint4 xf[G::KS];
   load_x(tile, xf);
@@ -170,7 +172,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
         const uint4 hv = hvk_pack8(v);
-        hvk_st16(yp + 32 * j, hv);
+        if (EPI == 1 && (HVK_NT_SAVED & 1))
+          hvk_st16_nt(yp + 32 * j, hv);
+        else
+          hvk_st16(yp + 32 * j, hv);
         if (EPI == 1) {
           float u[8];
           hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference

@@ -21,6 +21,9 @@
 #ifndef HVK_GEMM_PROBE
 #define HVK_GEMM_PROBE 0
 #endif
+#ifndef HVK_TILE_PRIO  // A/B build: s_setprio 1 over each k-step's MFMAs
+#define HVK_TILE_PRIO 0
+#endif
 #if HVK_GEMM_PROBE == 4
 __device__ unsigned long long g_gemm_probe[32768 * 6];
 #endif
@@ -92,7 +95,8 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
       if (row >= M) row = M - 1;
 #pragma unroll
       for (int j = 0; j < NT / 2; ++j)
-        hp[b][j] = *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq);
+        hp[b][j] = (HVK_NT_SAVED & 8) ? hvk_ld16_nt(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq)
+                                      : *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq);
     }
   }
   hvk_u32x4 pk[MT][NT / 2], pg[EPI == 1 ? MT : 1][NT / 2];
@@ -140,7 +144,10 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
 #pragma unroll
     for (int j = 0; j < NT / 2; ++j) {
       const size_t o = (size_t)row * N + col0 + 32 * j + 8 * gq;
-      *reinterpret_cast<hvk_u32x4*>(Y + o) = pk[b][j];
+      if (EPI == 1 && (HVK_NT_SAVED & 1))  // h: read again only by the backward
+        __builtin_nontemporal_store(pk[b][j], reinterpret_cast<hvk_u32x4*>(Y + o));
+      else
+        *reinterpret_cast<hvk_u32x4*>(Y + o) = pk[b][j];
       if (EPI == 1) *reinterpret_cast<hvk_u32x4*>(Y2 + o) = pg[b][j];
     }
   }
@@ -263,9 +270,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
       read_half(0);
       read_half(1);
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(TN + 4) : "memory");
+      if (HVK_TILE_PRIO) __builtin_amdgcn_s_setprio(1);
       mfma_half(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       mfma_half(1);
+      if (HVK_TILE_PRIO) __builtin_amdgcn_s_setprio(0);
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {

@@ -103,6 +103,22 @@ __device__ __forceinline__ void hvk_st16(void* p, uint4 v) {
   __builtin_nontemporal_store(__builtin_bit_cast(hvk_u32x4, v), reinterpret_cast<hvk_u32x4*>(p));
 #endif
 }
+// Always-nontemporal 16-B accesses for data nobody touches again soon, so it does not evict
+// what the NEXT kernel reads (the 4 MB L2s and the 256 MB Infinity Cache hold a stage-2
+// tensor): HVK_NT_SAVED bit 0: the fc1 pre-activation h (read again only in the backward);
+// bit 1: the LayerNorm's f32 residual stream (read again only at the next LayerNorm);
+// bit 2: the LayerNorm backward's f32 residual gradient (likewise); bit 3: the backward's one
+// read of h in the GELU' epilogues.  Default 7: bits 0+1 +0.7 % per step, bit 2 +0.2 % on
+// top, bit 3 neutral to -0.3 % (interleaved A/B, profiles/round2/nt_saved_ab.txt)
+#ifndef HVK_NT_SAVED
+#define HVK_NT_SAVED 7
+#endif
+__device__ __forceinline__ void hvk_st16_nt(void* p, uint4 v) {
+  __builtin_nontemporal_store(__builtin_bit_cast(hvk_u32x4, v), reinterpret_cast<hvk_u32x4*>(p));
+}
+__device__ __forceinline__ uint4 hvk_ld16_nt(const void* p) {
+  return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const hvk_u32x4*>(p)));
+}
 __device__ __forceinline__ void hvk_st8(void* p, uint2 v) {
 #ifndef HVK_NT
   *reinterpret_cast<uint2*>(p) = v;

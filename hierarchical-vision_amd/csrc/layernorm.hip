@@ -108,7 +108,15 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
       }
 #pragma unroll
       for (int j = 0; j < EPT; ++j) r[j] += ((v[j] - mu) * rs * gm[j] + bt[j]) * sc;
-      store_f32<EPT>(p.x + (size_t)row * p.C + c0, r);
+      if (HVK_NT_SAVED & 2) {  // the f32 stream is read again only at the next LayerNorm
+#pragma unroll
+        for (int i = 0; i < EPT / 4; ++i)
+          hvk_st16_nt(p.x + (size_t)row * p.C + c0 + 4 * i,
+                      make_uint4(__float_as_uint(r[4 * i]), __float_as_uint(r[4 * i + 1]),
+                                 __float_as_uint(r[4 * i + 2]), __float_as_uint(r[4 * i + 3])));
+      } else {
+        store_f32<EPT>(p.x + (size_t)row * p.C + c0, r);
+      }
       if (p.xb) store_bf16<EPT>(p.xb + (size_t)row * p.C + c0, r);
       if (t == 0) { p.mean[row] = mu; p.rstd[row] = rs; }
     }
@@ -189,7 +197,17 @@ __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
         dab[j] += d[j];
       }
       store_bf16<EPT>(p.ga + (size_t)row * p.C + c0, d);
-      if (p.gx0) store_f32<EPT>(p.gx0 + (size_t)row * p.C + c0, go);
+      if (p.gx0) {
+        if (HVK_NT_SAVED & 4) {
+#pragma unroll
+          for (int i = 0; i < EPT / 4; ++i)
+            hvk_st16_nt(p.gx0 + (size_t)row * p.C + c0 + 4 * i,
+                        make_uint4(__float_as_uint(go[4 * i]), __float_as_uint(go[4 * i + 1]),
+                                   __float_as_uint(go[4 * i + 2]), __float_as_uint(go[4 * i + 3])));
+        } else {
+          store_f32<EPT>(p.gx0 + (size_t)row * p.C + c0, go);
+        }
+      }
     }
   }
   // fold the RPW row slots of the wave (lanes t, t+TPR, ...), then the waves via LDS
