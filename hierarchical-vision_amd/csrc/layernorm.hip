@@ -20,11 +20,14 @@ namespace {
 
 constexpr int kWaves = 4;
 
+// HVK_NT_SAVED bit 4: the LayerNorm kernels' streamed inputs (the GEMM output a, the f32
+// residual stream / its gradient, the bf16 gradient) are read for the last time in the pass
+// (a again only by the backward), so they are loaded nontemporally
 template <int EPT>
 __device__ __forceinline__ void load_bf16(const hvk_bf16* p, float v[EPT]) {
 #pragma unroll
   for (int i = 0; i < EPT / 8; ++i) {
-    const uint4 w = reinterpret_cast<const uint4*>(p)[i];
+    const uint4 w = (HVK_NT_SAVED & 16) ? hvk_ld16_nt(p + 8 * i) : reinterpret_cast<const uint4*>(p)[i];
     float f[8];
     hvk_unpack8(w, f);
 #pragma unroll
@@ -41,6 +44,19 @@ __device__ __forceinline__ void load_f32(const float* p, float v[EPT]) {
 #pragma unroll
   for (int i = 0; i < EPT / 4; ++i) {
     const float4 w = reinterpret_cast<const float4*>(p)[i];
+    v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
+  }
+}
+template <int EPT>
+__device__ __forceinline__ void load_f32_stream(const float* p, float v[EPT]) {
+  if (!(HVK_NT_SAVED & 16)) {
+    load_f32<EPT>(p, v);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < EPT / 4; ++i) {
+    const uint4 u = hvk_ld16_nt(p + 4 * i);
+    const float4 w = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
     v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
   }
 }
@@ -101,7 +117,7 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
     if (act) {
       const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
       float r[EPT];
-      if (p.x0) load_f32<EPT>(p.x0 + (size_t)row * p.C + c0, r);
+      if (p.x0) load_f32_stream<EPT>(p.x0 + (size_t)row * p.C + c0, r);
       else {
 #pragma unroll
         for (int j = 0; j < EPT; ++j) r[j] = 0.f;
@@ -162,7 +178,7 @@ __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
     if (act) {
       load_bf16<EPT>(p.a + (size_t)row * p.C + c0, y);
-      if (p.gx) load_f32<EPT>(p.gx + (size_t)row * p.C + c0, go);
+      if (p.gx) load_f32_stream<EPT>(p.gx + (size_t)row * p.C + c0, go);
       else {
 #pragma unroll
         for (int j = 0; j < EPT; ++j) go[j] = 0.f;

@@ -331,10 +331,17 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
       nrow[i] = window_token_row(g, b, wh, ww, WIN, t < K::N ? t : 0);
       if (t < K::N) {
         const hvk_bf16* p = a.qkv + (size_t)nrow[i] * C3 + h * 32 + 8 * gq;
-        qf[i] = hvk_ld16(p);
-        kf[i] = hvk_ld16(p + C);
-        vf[i] = hvk_ld16(p + 2 * C);
-        df[i] = hvk_ld16(a.dout + (size_t)nrow[i] * C + h * 32 + 8 * gq);
+        if (HVK_NT_SAVED & 32) {  // the last read of qkv and of dO
+          qf[i] = hvk_ld16_nt(p);
+          kf[i] = hvk_ld16_nt(p + C);
+          vf[i] = hvk_ld16_nt(p + 2 * C);
+          df[i] = hvk_ld16_nt(a.dout + (size_t)nrow[i] * C + h * 32 + 8 * gq);
+        } else {
+          qf[i] = hvk_ld16(p);
+          kf[i] = hvk_ld16(p + C);
+          vf[i] = hvk_ld16(p + 2 * C);
+          df[i] = hvk_ld16(a.dout + (size_t)nrow[i] * C + h * 32 + 8 * gq);
+        }
       } else {
         qf[i] = kf[i] = vf[i] = df[i] = make_uint4(0, 0, 0, 0);
       }
