@@ -234,10 +234,12 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict
       const float4 v = red[j][tx];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    if (e < ndw4)
-      dw[e] = s;
+    float4* dst = e < ndw4 ? dw + e : db + (e - ndw4);
+    if (HVK_NT_SAVED & 64)  // read only by the optimizer at the end of the step
+      hvk_st16_nt(dst, make_uint4(__float_as_uint(s.x), __float_as_uint(s.y), __float_as_uint(s.z),
+                                  __float_as_uint(s.w)));
     else
-      db[e - ndw4] = s;
+      *dst = s;
   }
 }
 

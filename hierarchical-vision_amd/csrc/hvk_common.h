@@ -109,7 +109,8 @@ __device__ __forceinline__ void hvk_st16(void* p, uint4 v) {
 // bit 1: the LayerNorm's f32 residual stream (read again only at the next LayerNorm);
 // bit 2: the LayerNorm backward's f32 residual gradient (likewise); bit 3: the backward's one
 // read of h in the GELU' epilogues; bit 4: the LayerNorm kernels' streamed loads; bit 5: the
-// W-MSA backward's q/k/v/dO loads.  Default 7: bits 0+1 +0.7 % per step, bit 2 +0.2 % on top,
+// W-MSA backward's q/k/v/dO loads; bit 6: the f32 weight / bias gradients (read only by the
+// optimizer at the end of the step; neutral, off).  Default 7: bits 0+1 +0.7 % per step, bit 2 +0.2 % on top,
 // bit 3 neutral to -0.3 %, bit 4 -0.4 %, bit 5 -0.5 % (its kernel 185 -> 190 us): loads that
 // hit the Infinity Cache lose the hit (interleaved A/B, profiles/round2/nt_saved_ab.txt)
 #ifndef HVK_NT_SAVED
