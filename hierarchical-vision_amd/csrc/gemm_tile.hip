@@ -571,7 +571,12 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
     const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
     if (r >= 0) return r;
   }
-  const bool wide = N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536));
+  // the fused fc1 + GELU epilogue (EPI 1) at K >= 384 (stages 2-3) prefers 128-column tiles:
+  // half the per-tile epilogue, which the co-resident workgroup then hides better
+  // (tools/gpu_tilew.sh: 2-7 % on s2/s3 fc1; 192 stays faster for stage-1 fc1 and for EPI 2)
+  const bool epi1_narrow = EPI == 1 && K >= 384 && N % TileCfg<4>::BN == 0;
+  const bool wide = N % TileCfg<6>::BN == 0 &&
+                    (force >= 0 ? force == 1 : ((N > 384 || K >= 1536) && !epi1_narrow));
   if (N % TileCfg<4>::BN == 0 && !wide)
     return tile_pipe() ? launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st)
                        : launch_tile_<EPI, false, 4>(X, W, bias, Y, Y2, M, N, K, st);
