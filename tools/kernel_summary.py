@@ -30,6 +30,14 @@ CATS = [  # (category, regex on the kernel name), first match wins
 ]
 
 
+def category(name):
+    """The CATS category of a kernel name (first match), else "other"."""
+    for c, rx in CATS:
+        if re.search(rx, name):
+            return c
+    return "other"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
