@@ -212,6 +212,120 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
   }
 }
 
+// Fused MLP forward for the stage-0 width (swinv2.py:58-65, C = 96, hidden 384): fc1 + bias +
+// GELU and fc2 in one persistent kernel.  W1 [384 x 96] and W2 [96 x 384] both stay in LDS
+// (2 x 72 KB, one 8-wave workgroup per CU); per 16-token tile a wave computes h^T = W1 x^T
+// (24 tiles), writes h (nontemporal: read again only by the backward) and GELU(h) (saved for
+// fc2's weight gradient) exactly as linear_kernel<96, 384, EPI 1> does, and feeds GELU(h)
+// straight from registers into y^T = W2 GELU(h)^T: with W1's rows permuted (perm_row) a lane
+// holds hidden units 32j + 8g .. +7 of its token, which IS the B fragment of fc2's k-chunk j,
+// so the chain needs no data movement and fc2 accumulates its 12 chunks in the same order as
+// linear_kernel<384, 96> (bit-identical y).  Saves fc2's re-read of GELU(h) (616 MB per block
+// at bs256).
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __restrict__ X,
+                                                           const hvk_bf16* __restrict__ W1,
+                                                           const float* __restrict__ b1,
+                                                           const hvk_bf16* __restrict__ W2,
+                                                           const float* __restrict__ b2,
+                                                           hvk_bf16* __restrict__ H,
+                                                           hvk_bf16* __restrict__ Gh,
+                                                           hvk_bf16* __restrict__ Y, int M,
+                                                           int row_groups) {
+  using G1 = GCfg<96, 384>;   // fc1: K 96, 384 outputs
+  using G2 = GCfg<384, 96>;   // fc2: K 384, 96 outputs
+  constexpr int K = 96, N1 = 384, N2 = 96, kThreads = 64 * WAVES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* w1l = reinterpret_cast<uint4*>(smem);                                      // [24][12][16]
+  uint4* w2l = reinterpret_cast<uint4*>(smem + (size_t)N1 * G1::U4 * 16);            // [6][48][16]
+  float* b1l = reinterpret_cast<float*>(smem + (size_t)N1 * G1::U4 * 16 + (size_t)N2 * G2::U4 * 16);
+  float* b2l = b1l + N1;
+  for (int e = threadIdx.x; e < N1 * G1::U4; e += kThreads) {
+    const int p = e / G1::U4, u = e % G1::U4;
+    w1l[((p >> 4) * G1::U4 + u) * 16 + (p & 15)] =
+        *reinterpret_cast<const uint4*>(W1 + (size_t)perm_row(p) * K + 8 * u);
+  }
+  for (int e = threadIdx.x; e < N2 * G2::U4; e += kThreads) {
+    const int p = e / G2::U4, u = e % G2::U4;
+    w2l[((p >> 4) * G2::U4 + u) * 16 + (p & 15)] =
+        *reinterpret_cast<const uint4*>(W2 + (size_t)perm_row(p) * N1 + 8 * u);
+  }
+  for (int e = threadIdx.x; e < N1; e += kThreads) b1l[e] = b1[e];
+  for (int e = threadIdx.x; e < N2; e += kThreads) b2l[e] = b2 ? b2[e] : 0.f;
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tiles = (M + 15) >> 4;
+  const int stride = row_groups * WAVES;
+  int tile = blockIdx.x * WAVES + wave;
+  auto load_x = [&](int t, uint4 (&xf)[G1::KS]) {
+    const int row = 16 * t + li;
+    const bool ok = t < tiles && row < M;
+    const hvk_bf16* xp = X + (size_t)row * K + 8 * g;
+#pragma unroll
+    for (int s = 0; s < G1::KS; ++s) xf[s] = ok ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+  };
+  uint4 xf[G1::KS];
+  load_x(tile, xf);
+  for (; tile < tiles; tile += stride) {
+    asm volatile("" ::: "memory");
+    uint4 xn[G1::KS];
+    load_x(tile + stride, xn);
+    hvk_f32x4 acc[G1::NT];
+#pragma unroll
+    for (int t = 0; t < G1::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < G1::KS; ++s)
+#pragma unroll
+      for (int t = 0; t < G1::NT; ++t) acc[t] = hvk_mfma16(w1l[(t * G1::U4 + 4 * s + g) * 16 + li], xf[s], acc[t]);
+    const int row = 16 * tile + li;
+    const bool ok = row < M;
+    hvk_f32x4 acc2[G2::NT];
+#pragma unroll
+    for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < G1::NT / 2; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[2 * j][r] + b1l[32 * j + 8 * g + r];
+        v[4 + r] = acc[2 * j + 1][r] + b1l[32 * j + 8 * g + 4 + r];
+      }
+      const uint4 hv = hvk_pack8(v);
+      const uint4 gv = hvk_gelu8_bf16(hv);  // GELU of the rounded pre-activation, as the reference
+      if (ok) {
+        const size_t o = (size_t)row * N1 + 32 * j + 8 * g;
+        if (HVK_NT_SAVED & 1)
+          hvk_st16_nt(H + o, hv);
+        else
+          hvk_st16(H + o, hv);
+        hvk_st16(Gh + o, gv);
+      }
+      // fc2 k-chunk j: this lane's GELU(h) of hidden units 32j + 8g .. +7 is the B fragment
+#pragma unroll
+      for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
+    }
+    if (ok) {
+#pragma unroll
+      for (int j = 0; j < G2::NT / 2; ++j) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc2[2 * j][r];
+          v[4 + r] = acc2[2 * j + 1][r];
+        }
+        if (b2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += b2l[32 * j + 8 * g + e];
+        }
+        hvk_st16(Y + (size_t)row * N2 + 32 * j + 8 * g, hvk_pack8(v));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
+  }
+}
+
 int g_cu_count = 0;
 
 template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
@@ -354,6 +468,41 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   if (K == 128) return launch_linear<128, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   if (K == 256) return launch_linear<256, 128, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
+}
+
+int hvk_mlp_fwd_supported(int M, int K, int N1, int N2) { return M > 0 && K == 96 && N1 == 384 && N2 == 96; }
+
+int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                void* g, void* y, int M, int K, int N1, int N2, void* stream) {
+  if (!x || !w1 || !b1 || !w2 || !h || !g || !y) return hvk_set_error(HVK_EINVAL, "hvk_mlp_fwd: null pointer");
+  if (!hvk_mlp_fwd_supported(M, K, N1, N2))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_fwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
+  constexpr int WAVES = 8;
+  constexpr size_t LDS = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16 + (384 + 96) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_fwd_kernel<WAVES>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+    attr = true;
+  }
+  if (!g_cu_count) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_mlp_fwd: device query failed");
+    g_cu_count = prop.multiProcessorCount;
+  }
+  const int tiles = (M + 15) / 16;
+  int groups = g_cu_count;  // one resident workgroup per CU (LDS)
+  const int need = (tiles + WAVES - 1) / WAVES;
+  if (groups > need) groups = need;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_fwd_kernel<WAVES>), dim3(groups),
+                     dim3(64 * WAVES), LDS, st, static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w1),
+                     b1, static_cast<const hvk_bf16*>(w2), b2, static_cast<hvk_bf16*>(h),
+                     static_cast<hvk_bf16*>(g), static_cast<hvk_bf16*>(y), M, groups);
+  HVK_CHECK_LAUNCH("hvk_mlp_fwd");
+  return HVK_OK;
 }
 
 int hvk_linear_gelu_in_supported(int M, int K, int N) { return M > 0 && K == 384 && N == 96; }

@@ -714,6 +714,9 @@ def linear_gelu(x, weight, bias):
     return bias_gelu(linear(x, weight), bias)
 
 
+_MLP_FUSED = os.environ.get("HVK_MLP_FUSED", "1") != "0"  # 0: fc1+GELU and fc2 as two launches (A/B)
+
+
 class MlpFn(torch.autograd.Function):
     """fc2(GELU(fc1(x))) (swinv2.py:58-65 with drop = 0): forward = the fused fc1 + GELU kernel
     and the fc2 GEMM; backward runs fc2's input gradient and the activation backward as ONE
@@ -740,6 +743,15 @@ class MlpFn(torch.autograd.Function):
             call("hvk_linear_gelu_in_fwd", ptr(h), ptr(w2b), ptr(b) if b is not None else None, ptr(y), M,
                  N1, N2, stream())
             ctx.save_for_backward(xb, w1b, w2b, h)
+        elif _MLP_FUSED and _lib.load().hvk_mlp_fwd_supported(M, K, N1, N2):
+            # stage-0 width: fc1 + GELU + fc2 in one kernel (no re-read of GELU(h))
+            h = torch.empty((M, N1), device=x2.device, dtype=torch.bfloat16)
+            y1 = torch.empty_like(h)
+            y = torch.empty((M, N2), device=x2.device, dtype=torch.bfloat16)
+            b = _f32(b2) if b2 is not None else None
+            call("hvk_mlp_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(w2b), ptr(b) if b is not None else None,
+                 ptr(h), ptr(y1), ptr(y), M, K, N1, N2, stream())
+            ctx.save_for_backward(xb, w1b, w2b, h, y1)
         else:
             h, y1 = gelu_fwd(x2, w1b, b1)
             y = mm_nt(y1, w2b, b2)

@@ -103,6 +103,14 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
  * dbias: f32 [N] or NULL, ACCUMULATED into (+= column sums of gh = the fc1 bias gradient;
  * the caller zeroes it).  Replaces the input-gradient GEMM + activation backward + bias reduction for
  * the (K, N) shapes hvk_linear_gelu_bwd_supported() reports. */
+/* The whole MLP forward of the stage-0 width (swinv2.py:58-65, C = 96, hidden 384) in one
+ * kernel: h = bf16(x w1^T + b1) (saved for the backward), g = GELU(h) (saved for fc2's weight
+ * gradient), y = bf16(g w2^T (+ b2)); bit-identical to hvk_linear_gelu_fwd followed by
+ * hvk_linear_fwd(g, w2, b2) without fc2's re-read of g.  x [M, 96], w1 [384, 96], w2 [96, 384]
+ * bf16; b1 f32 [384] required, b2 f32 [96] or NULL; h, g [M, 384], y [M, 96] bf16. */
+int hvk_mlp_fwd_supported(int M, int K, int N1, int N2);
+int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                void* g, void* y, int M, int K, int N1, int N2, void* stream);
 /* fc2 forward on the saved pre-activation: y = GELU(h) w^T (+ bias), GELU recomputed per
  * loaded fragment exactly as hvk_linear_gelu_fwd stores it (swinv2.py:58-65).  Built for
  * K = 384, N = 96 (stage 0). */

@@ -397,3 +397,36 @@ def test_gemm_pingpong_bit_identical_to_two_wg_kernel(M, K, N, epi):
         torch.nn.functional.gelu(hf).backward(ref)
         ref = hf.grad
     assert ((y1.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M", [802816, 1000, 37])
+@pytest.mark.parametrize("with_b2", [False, True])
+def test_fused_mlp_forward_bit_identical(M, with_b2):
+    """hvk_mlp_fwd (stage-0 MLP forward in one kernel) == hvk_linear_gelu_fwd + hvk_linear_fwd on
+    the same operands, bit for bit (h, GELU(h) and y), ragged M included; and y within 1e-2 of
+    fp32 math on the same bf16 operands."""
+    from hvamd import _lib
+    lib = _lib.load()
+    K, N1, N2 = 96, 384, 96
+    assert lib.hvk_mlp_fwd_supported(M, K, N1, N2)
+    gen = torch.Generator(device="cuda").manual_seed(M + int(with_b2))
+    x = torch.randn(M, K, device="cuda", generator=gen).bfloat16()
+    w1 = (torch.randn(N1, K, device="cuda", generator=gen) / K ** 0.5).bfloat16()
+    b1 = torch.randn(N1, device="cuda", generator=gen) * 0.1
+    w2 = (torch.randn(N2, N1, device="cuda", generator=gen) / N1 ** 0.5).bfloat16()
+    b2 = torch.randn(N2, device="cuda", generator=gen) * 0.1 if with_b2 else None
+    P = _lib.ptr
+    h0, g0 = (torch.empty(M, N1, device="cuda", dtype=torch.bfloat16) for _ in range(2))
+    y0 = torch.empty(M, N2, device="cuda", dtype=torch.bfloat16)
+    _lib.call("hvk_linear_gelu_fwd", P(x), P(w1), P(b1), P(h0), P(g0), M, K, N1, _lib.stream())
+    _lib.call("hvk_linear_fwd", P(g0), P(w2), P(b2), P(y0), M, N1, N2, _lib.stream())
+    h1, g1 = (torch.full((M, N1), float("nan"), device="cuda", dtype=torch.bfloat16) for _ in range(2))
+    y1 = torch.full((M, N2), float("nan"), device="cuda", dtype=torch.bfloat16)
+    _lib.call("hvk_mlp_fwd", P(x), P(w1), P(b1), P(w2), P(b2), P(h1), P(g1), P(y1), M, K, N1, N2, _lib.stream())
+    torch.cuda.synchronize()
+    for a, b in ((h0, h1), (g0, g1), (y0, y1)):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    if M <= 1000:
+        ref = torch.nn.functional.gelu((x.float() @ w1.float().t() + b1).bfloat16().float()) @ w2.float().t()
+        ref = ref + (b2 if with_b2 else 0)
+        assert ((y1.float() - ref).norm() / ref.norm()).item() < 1e-2
