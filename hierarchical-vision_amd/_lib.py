@@ -57,6 +57,8 @@ SIGNATURES = {
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
     "hvk_mlp_fwd_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "hvk_mlp_bwd_supported": (_i, [_i, _i, _i, _i]),
+    "hvk_mlp_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
     "hvk_linear_gelu_in_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_in_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_weight_grad_gelu_x_supported": (_i, [_i, _i, _i]),

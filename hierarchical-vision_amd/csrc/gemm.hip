@@ -326,6 +326,122 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
   }
 }
 
+// Fused MLP input-gradient chain for the stage-0 width (the backward of swinv2.py:58-65 at
+// C = 96): gh = bf16((gy w2t^T) * GELU'(h)) (linear_kernel<96, 128, EPI 2>'s math) and
+// gx = gh w1t^T (linear_kernel<384, 96>'s), one persistent kernel with w2t [384 x 96] and
+// w1t [96 x 384] in LDS.  Per 16-token tile a wave produces gh in three 128-column chunks; each
+// chunk is stored (fc1's weight gradient reads it) and fed from registers into gx's k-chunks
+// 4q .. 4q+3 (same layout argument as mlp_fwd_kernel), so fc1's input gradient does not
+// re-read gh (616 MB per block at bs256).  Bit-identical to the two launches it replaces.
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __restrict__ GY,
+                                                           const hvk_bf16* __restrict__ W2t,
+                                                           const hvk_bf16* __restrict__ Hs,
+                                                           const hvk_bf16* __restrict__ W1t,
+                                                           hvk_bf16* __restrict__ GH,
+                                                           hvk_bf16* __restrict__ GX, int M,
+                                                           int row_groups) {
+  using G1 = GCfg<96, 384>;   // gh: K 96, 384 outputs
+  using G2 = GCfg<384, 96>;   // gx: K 384, 96 outputs
+  constexpr int K = 96, N1 = 384, N2 = 96, kThreads = 64 * WAVES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* w1l = reinterpret_cast<uint4*>(smem);                                   // w2t [24][12][16]
+  uint4* w2l = reinterpret_cast<uint4*>(smem + (size_t)N1 * G1::U4 * 16);         // w1t [6][48][16]
+  for (int e = threadIdx.x; e < N1 * G1::U4; e += kThreads) {
+    const int p = e / G1::U4, u = e % G1::U4;
+    w1l[((p >> 4) * G1::U4 + u) * 16 + (p & 15)] =
+        *reinterpret_cast<const uint4*>(W2t + (size_t)perm_row(p) * K + 8 * u);
+  }
+  for (int e = threadIdx.x; e < N2 * G2::U4; e += kThreads) {
+    const int p = e / G2::U4, u = e % G2::U4;
+    w2l[((p >> 4) * G2::U4 + u) * 16 + (p & 15)] =
+        *reinterpret_cast<const uint4*>(W1t + (size_t)perm_row(p) * N1 + 8 * u);
+  }
+  __syncthreads();
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int tiles = (M + 15) >> 4;
+  const int stride = row_groups * WAVES;
+  int tile = blockIdx.x * WAVES + wave;
+  auto load_x = [&](int t, uint4 (&xf)[G1::KS]) {
+    const int row = 16 * t + li;
+    const bool ok = t < tiles && row < M;
+    const hvk_bf16* xp = GY + (size_t)row * K + 8 * g;
+#pragma unroll
+    for (int s = 0; s < G1::KS; ++s) xf[s] = ok ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+  };
+  auto load_h = [&](int t, uint4 (&hf)[G1::NT / 2]) {
+    const int row = 16 * t + li;
+    const bool ok = t < tiles && row < M;
+#pragma unroll
+    for (int j = 0; j < G1::NT / 2; ++j)
+      hf[j] = ok ? hvk_ld16(Hs + (size_t)row * N1 + 32 * j + 8 * g) : make_uint4(0, 0, 0, 0);
+  };
+  uint4 xf[G1::KS], hf[G1::NT / 2];
+  load_x(tile, xf);
+  load_h(tile, hf);
+  for (; tile < tiles; tile += stride) {
+    asm volatile("" ::: "memory");
+    uint4 xn[G1::KS], hn[G1::NT / 2];
+    load_x(tile + stride, xn);
+    load_h(tile + stride, hn);
+    const int row = 16 * tile + li;
+    const bool ok = row < M;
+    hvk_f32x4 acc2[G2::NT];
+#pragma unroll
+    for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {  // gh columns 128q .. 128q + 127 (W tiles 8q .. 8q + 7)
+      hvk_f32x4 acc[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < G1::KS; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          acc[t] = hvk_mfma16(w1l[((8 * q + t) * G1::U4 + 4 * s + g) * 16 + li], xf[s], acc[t]);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * q + jj;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc[2 * jj][r];
+          v[4 + r] = acc[2 * jj + 1][r];
+        }
+        float hv[8];
+        hvk_unpack8(hf[j], hv);
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const hvk_gelu::f32x2 d = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hv[e], hv[e + 1]});
+          v[e] *= d.x;
+          v[e + 1] *= d.y;
+        }
+        const uint4 gv = hvk_pack8(v);
+        if (ok) hvk_st16(GH + (size_t)row * N1 + 32 * j + 8 * g, gv);
+#pragma unroll
+        for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
+      }
+    }
+    if (ok) {
+#pragma unroll
+      for (int j = 0; j < G2::NT / 2; ++j) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = acc2[2 * j][r];
+          v[4 + r] = acc2[2 * j + 1][r];
+        }
+        hvk_st16(GX + (size_t)row * N2 + 32 * j + 8 * g, hvk_pack8(v));
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
+#pragma unroll
+    for (int j = 0; j < G1::NT / 2; ++j) hf[j] = hn[j];
+  }
+}
+
 int g_cu_count = 0;
 
 template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
@@ -502,6 +618,41 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
                      b1, static_cast<const hvk_bf16*>(w2), b2, static_cast<hvk_bf16*>(h),
                      static_cast<hvk_bf16*>(g), static_cast<hvk_bf16*>(y), M, groups);
   HVK_CHECK_LAUNCH("hvk_mlp_fwd");
+  return HVK_OK;
+}
+
+int hvk_mlp_bwd_supported(int M, int K, int N1, int N2) { return M > 0 && K == 96 && N1 == 384 && N2 == 96; }
+
+int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t, void* gh, void* gx, int M,
+                int K, int N1, int N2, void* stream) {
+  if (!gy || !w2t || !h || !w1t || !gh || !gx) return hvk_set_error(HVK_EINVAL, "hvk_mlp_bwd: null pointer");
+  if (!hvk_mlp_bwd_supported(M, K, N1, N2))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_bwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
+  constexpr int WAVES = 8;
+  constexpr size_t LDS = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_bwd_kernel<WAVES>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+    attr = true;
+  }
+  if (!g_cu_count) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return hvk_set_error(HVK_EHIP, "hvk_mlp_bwd: device query failed");
+    g_cu_count = prop.multiProcessorCount;
+  }
+  const int tiles = (M + 15) / 16;
+  int groups = g_cu_count;
+  const int need = (tiles + WAVES - 1) / WAVES;
+  if (groups > need) groups = need;
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_bwd_kernel<WAVES>), dim3(groups),
+                     dim3(64 * WAVES), LDS, static_cast<hipStream_t>(stream), static_cast<const hvk_bf16*>(gy),
+                     static_cast<const hvk_bf16*>(w2t), static_cast<const hvk_bf16*>(h),
+                     static_cast<const hvk_bf16*>(w1t), static_cast<hvk_bf16*>(gh), static_cast<hvk_bf16*>(gx),
+                     M, groups);
+  HVK_CHECK_LAUNCH("hvk_mlp_bwd");
   return HVK_OK;
 }
 

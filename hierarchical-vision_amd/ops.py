@@ -775,6 +775,15 @@ class MlpFn(torch.autograd.Function):
             dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
         w2t = _bf16_t(w2b, ctx.wts[1])
+        if (_MLP_FUSED and ctx.needs_input_grad[0] and not ctx.recompute
+                and _lib.load().hvk_mlp_bwd_supported(M, N2, N1, K)):
+            # stage-0 width: fc2's input gradient through GELU' and fc1's input gradient in one
+            # kernel (gh stored for fc1's weight gradient, not re-read for gx)
+            gx = torch.empty((M, K), device=h.device, dtype=torch.bfloat16)
+            call("hvk_mlp_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(_bf16_t(w1b, ctx.wts[0])), ptr(gh), ptr(gx),
+                 M, N2, N1, K, stream())
+            dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+            return gx.reshape(xb.shape), dw1, db1, dw2, db2
         if _tile_ok(M, N2, N1) and not (N2 in _SKINNY_FIRST and
                                          _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
             call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())

@@ -111,6 +111,14 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
 int hvk_mlp_fwd_supported(int M, int K, int N1, int N2);
 int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
                 void* g, void* y, int M, int K, int N1, int N2, void* stream);
+/* Its backward chain at the same width (the input gradients of swinv2.py:58-65): gh =
+ * bf16((gy w2t^T) * GELU'(h)) and gx = bf16(gh w1t^T) in one kernel, gh also stored (fc1's
+ * weight gradient reads it); bit-identical to hvk_linear_gelu_bwd + hvk_linear_fwd(gh, w1t)
+ * without the second kernel's re-read of gh.  gy [M, 96], w2t = fc2.weight^T [384, 96],
+ * h [M, 384], w1t = fc1.weight^T [96, 384]; gh [M, 384], gx [M, 96]. */
+int hvk_mlp_bwd_supported(int M, int K, int N1, int N2);
+int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t, void* gh, void* gx, int M,
+                int K, int N1, int N2, void* stream);
 /* fc2 forward on the saved pre-activation: y = GELU(h) w^T (+ bias), GELU recomputed per
  * loaded fragment exactly as hvk_linear_gelu_fwd stores it (swinv2.py:58-65).  Built for
  * K = 384, N = 96 (stage 0). */

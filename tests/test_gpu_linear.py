@@ -430,3 +430,35 @@ def test_fused_mlp_forward_bit_identical(M, with_b2):
         ref = torch.nn.functional.gelu((x.float() @ w1.float().t() + b1).bfloat16().float()) @ w2.float().t()
         ref = ref + (b2 if with_b2 else 0)
         assert ((y1.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("M", [802816, 1000, 37])
+def test_fused_mlp_input_gradients_bit_identical(M):
+    """hvk_mlp_bwd (stage-0 gh = (gy w2t^T) * GELU'(h) and gx = gh w1t^T in one kernel) ==
+    hvk_linear_gelu_bwd + hvk_linear_fwd on the same operands, bit for bit (gh and gx), ragged M
+    included; and gx within 1e-2 of fp32 autograd on the same bf16 operands."""
+    from hvamd import _lib
+    lib = _lib.load()
+    K, N1 = 96, 384
+    assert lib.hvk_mlp_bwd_supported(M, K, N1, K)
+    gen = torch.Generator(device="cuda").manual_seed(M + 5)
+    gy = torch.randn(M, K, device="cuda", generator=gen).bfloat16()
+    w2t = (torch.randn(N1, K, device="cuda", generator=gen) / K ** 0.5).bfloat16()
+    h = torch.randn(M, N1, device="cuda", generator=gen).bfloat16()
+    w1t = (torch.randn(K, N1, device="cuda", generator=gen) / N1 ** 0.5).bfloat16()
+    P = _lib.ptr
+    gh0 = torch.empty(M, N1, device="cuda", dtype=torch.bfloat16)
+    gx0 = torch.empty(M, K, device="cuda", dtype=torch.bfloat16)
+    _lib.call("hvk_linear_gelu_bwd", P(gy), P(w2t), P(h), P(gh0), None, M, K, N1, _lib.stream())
+    _lib.call("hvk_linear_fwd", P(gh0), P(w1t), None, P(gx0), M, N1, K, _lib.stream())
+    gh1 = torch.full((M, N1), float("nan"), device="cuda", dtype=torch.bfloat16)
+    gx1 = torch.full((M, K), float("nan"), device="cuda", dtype=torch.bfloat16)
+    _lib.call("hvk_mlp_bwd", P(gy), P(w2t), P(h), P(w1t), P(gh1), P(gx1), M, K, N1, K, _lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(gh0.view(torch.int16), gh1.view(torch.int16))
+    assert torch.equal(gx0.view(torch.int16), gx1.view(torch.int16))
+    if M <= 1000:
+        hf = h.float().requires_grad_(True)
+        torch.nn.functional.gelu(hf).backward(gy.float() @ w2t.float().t())
+        ref = hf.grad @ w1t.float().t()
+        assert ((gx1.float() - ref).norm() / ref.norm()).item() < 1e-2
