@@ -21,7 +21,7 @@ CATS = [  # (category, regex on the kernel name), first match wins
     ("patch_merge", r"merge_kernel"),
     ("losses", r"multitask|hxe"),
     ("gemm(dW)", r"dw_kernel|dw_reduce"),
-    ("gemm(hvk)", r"linear_kernel|gemm_nt_kernel"),
+    ("gemm(hvk)", r"linear_kernel|gemm_nt_kernel|gemm_pp_kernel|mlp_fwd_kernel|mlp_bwd_kernel"),
     ("gemm", r"Cijk|gemm|Gemm|GEMM|mfma|MT\d+x\d+"),
     ("memset", r"[Mm]emset|fill"),
     ("reduce", r"reduce|Reduce"),
