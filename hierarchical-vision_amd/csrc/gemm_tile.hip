@@ -21,6 +21,9 @@
 #ifndef HVK_GEMM_PROBE
 #define HVK_GEMM_PROBE 0
 #endif
+#ifndef HVK_TILE_HPRE  // 1: EPI 2's h loads issued two k-steps before the epilogue
+#define HVK_TILE_HPRE 1
+#endif
 #ifndef HVK_TILE_PRIO  // A/B build: s_setprio 1 over each k-step's MFMAs
 #define HVK_TILE_PRIO 0
 #endif
@@ -72,10 +75,29 @@ __device__ __forceinline__ uint4 tie(hvk_u32x4 v) {
 // loads first, every output packed, then all 16-B stores back to back: a register still read
 // by an outstanding store cannot be rewritten before vmcnt says so, and a load waited for
 // between stores would wait for every store before it (vmcnt counts in order).
-template <int EPI, int NT, int MT>
+// EPI 2's saved pre-activation h of a lane's outputs, in the output layout
+template <int EPI, int NT, int MT, int B0 = 0, int B1 = MT, int HM = MT>
+__device__ __forceinline__ void load_h_tile(uint4 (&hp)[EPI == 2 ? HM : 1][NT / 2], const hvk_bf16* __restrict__ Y2,
+                                            int M, int N, int row0, int col0) {
+  if (EPI != 2) return;
+  const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int b = B0; b < B1; ++b) {
+    int row = row0 + 16 * b + li;
+    if (row >= M) row = M - 1;
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j)
+      hp[b][j] = (HVK_NT_SAVED & 8) ? hvk_ld16_nt(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq)
+                                    : *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq);
+  }
+}
+
+template <int EPI, int NT, int MT, int HPRE = 0>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
-                                              int N, int row0, int col0) {
+                                              int N, int row0, int col0,
+                                              const uint4 (*hpre)[NT / 2] = nullptr) {
+  // HPRE: h of token tiles 0 .. HPRE-1 was loaded early by the caller (hpre)
   const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   float bv[NT / 2][8];
   if (EPI != 2 && bias) {
@@ -87,17 +109,13 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
       bv[j][4] = b1.x; bv[j][5] = b1.y; bv[j][6] = b1.z; bv[j][7] = b1.w;
     }
   }
-  uint4 hp[EPI == 2 ? MT : 1][NT / 2];
-  if (EPI == 2) {  // gh = (gy w) * GELU'(h): h (Y2) read in the output layout
+  uint4 hp[EPI == 2 ? MT : 1][NT / 2];  // gh = (gy w) * GELU'(h): h (Y2) in the output layout
+  if (EPI == 2) {
 #pragma unroll
-    for (int b = 0; b < MT; ++b) {
-      int row = row0 + 16 * b + li;
-      if (row >= M) row = M - 1;
+    for (int b = 0; b < HPRE; ++b)
 #pragma unroll
-      for (int j = 0; j < NT / 2; ++j)
-        hp[b][j] = (HVK_NT_SAVED & 8) ? hvk_ld16_nt(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq)
-                                      : *reinterpret_cast<const uint4*>(Y2 + (size_t)row * N + col0 + 32 * j + 8 * gq);
-    }
+      for (int j = 0; j < NT / 2; ++j) hp[b][j] = hpre[b][j];
+    load_h_tile<EPI, NT, MT, HPRE, MT>(hp, Y2, M, N, row0, col0);
   }
   hvk_u32x4 pk[MT][NT / 2], pg[EPI == 1 ? MT : 1][NT / 2];
 #pragma unroll
@@ -216,6 +234,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t0 = wall_clock64();
   unsigned long long t1 = 0;
 #endif
+  // EPI 2: the epilogue's h vectors are loaded at the top of k-step KT-2 (after its DMA wait;
+  // the last two k-steps issue no DMA, and the vmcnt(0) at the top of k-step KT-1 covers them),
+  // so their latency hides under the last k-steps instead of opening the epilogue
+  constexpr int HPB = (EPI == 2 && HVK_TILE_HPRE) ? 2 : 0;  // token tiles prefetched (VGPR budget)
+  uint4 hpre[HPB ? HPB : 1][TN / 2];
+  const int hk = KT >= 2 ? KT - 2 : 0;
   issue(0, 0);
   if (KT > 1) issue(1, 1);
   for (int kt = 0; kt < KT; ++kt) {
@@ -224,6 +248,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(TN + 4) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (HPB && kt == hk)
+      load_h_tile<EPI, TN, 4, 0, HPB, HPB ? HPB : 1>(hpre, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 #if HVK_GEMM_PROBE == 4
@@ -293,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  tile_epilogue<EPI, TN, 4>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn);
+  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
