@@ -10,7 +10,8 @@ import glob
 import json
 import sys
 
-KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_kernel"}
+KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_kernel",
+           "mlp_fwd": "mlp_fwd_kernel", "mlp_bwd": "mlp_bwd_kernel"}  # the last two: fused stage-0 MLP
 
 
 def per_kernel(d, counter):
