@@ -88,6 +88,7 @@ SIGNATURES = {
 }
 
 _lib = None
+ABI_VERSION = 7  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
 
 
 def load():
@@ -99,6 +100,13 @@ def load():
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
                 "g.build()'` (or `make -C hierarchical-vision_amd/csrc`).  There is no fallback.")
         lib = ctypes.CDLL(LIB_PATH)
+        # an older build (an A/B variant through HVK_LIB_PATH) may export the same names with
+        # other argument lists: calling those would shift pointers, so refuse it outright
+        lib.hvk_abi_version.restype = _i
+        abi = lib.hvk_abi_version()
+        if abi != ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH} has C ABI {abi}, this binding expects {ABI_VERSION}: "
+                               "rebuild it (make -C hierarchical-vision_amd/csrc)")
         for name, (res, args) in SIGNATURES.items():
             # an older A/B build (HVK_LIB_PATH) may predate an entry point; the shipped one may not
             fn = getattr(lib, name, None)

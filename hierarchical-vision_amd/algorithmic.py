@@ -119,6 +119,16 @@ class GradientClipping(Algorithm):
             # computed on the device in the fused update, no host synchronisation)
             opt.pending_clip = self.clipping_threshold
             return
+        # clipping here, not in the optimizer: a DDP mean still pending as the optimizer's
+        # gradient scale (trainer._grad_mean hands 1/world over) must be applied first, or the
+        # threshold would act on world-times gradients
+        for o in opts:
+            scale = getattr(o, "pending_grad_scale", 1.0)
+            if scale != 1.0:
+                mine = [q.grad for g in o.param_groups for q in g["params"] if q.grad is not None]
+                if mine:
+                    torch._foreach_mul_(mine, float(scale))
+                o.pending_grad_scale = 1.0
         if self.clipping_type == "norm":
             torch.nn.utils.clip_grad_norm_(params, self.clipping_threshold, foreach=True)
         else:

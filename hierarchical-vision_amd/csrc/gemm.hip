@@ -586,7 +586,23 @@ int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h
   return launch_linear<192, 256, 8, true, 1>(X, W, bias, H, M, N, st, Yg);
 }
 
-int hvk_mlp_fwd_supported(int M, int K, int N1, int N2) { return M > 0 && K == 96 && N1 == 384 && N2 == 96; }
+namespace {
+constexpr size_t kMlpFwdLds = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16 + (384 + 96) * 4;
+constexpr size_t kMlpBwdLds = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16;
+// grant the fused MLP kernels their dynamic LDS (~149 KB) once; false when the device refuses
+// it (or there is no device), so the supported() predicates send the caller to the two-launch path
+bool mlp_lds_granted(const void* fn, size_t bytes, int& state) {
+  if (state == 0)
+    state = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess ? 1 : -1;
+  return state > 0;
+}
+int g_mlp_fwd_lds = 0, g_mlp_bwd_lds = 0;
+}  // namespace
+
+int hvk_mlp_fwd_supported(int M, int K, int N1, int N2) {
+  return M > 0 && K == 96 && N1 == 384 && N2 == 96 &&
+         mlp_lds_granted(reinterpret_cast<const void*>(&mlp_fwd_kernel<8>), kMlpFwdLds, g_mlp_fwd_lds);
+}
 
 int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
                 void* g, void* y, int M, int K, int N1, int N2, void* stream) {
@@ -594,13 +610,7 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
   if (!hvk_mlp_fwd_supported(M, K, N1, N2))
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_fwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
   constexpr int WAVES = 8;
-  constexpr size_t LDS = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16 + (384 + 96) * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_fwd_kernel<WAVES>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
-    attr = true;
-  }
+  constexpr size_t LDS = kMlpFwdLds;
   if (!g_cu_count) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -621,7 +631,10 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
   return HVK_OK;
 }
 
-int hvk_mlp_bwd_supported(int M, int K, int N1, int N2) { return M > 0 && K == 96 && N1 == 384 && N2 == 96; }
+int hvk_mlp_bwd_supported(int M, int K, int N1, int N2) {
+  return M > 0 && K == 96 && N1 == 384 && N2 == 96 &&
+         mlp_lds_granted(reinterpret_cast<const void*>(&mlp_bwd_kernel<8>), kMlpBwdLds, g_mlp_bwd_lds);
+}
 
 int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t, void* gh, void* gx, int M,
                 int K, int N1, int N2, void* stream) {
@@ -629,13 +642,7 @@ int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t,
   if (!hvk_mlp_bwd_supported(M, K, N1, N2))
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_bwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
   constexpr int WAVES = 8;
-  constexpr size_t LDS = (size_t)384 * GCfg<96, 384>::U4 * 16 + (size_t)96 * GCfg<384, 96>::U4 * 16;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_bwd_kernel<WAVES>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
-    attr = true;
-  }
+  constexpr size_t LDS = kMlpBwdLds;
   if (!g_cu_count) {
     int dev = 0;
     hipDeviceProp_t prop;

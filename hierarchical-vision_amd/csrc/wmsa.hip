@@ -658,11 +658,7 @@ size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
     const int n = window * window, nt = (n + 15) / 16;
     acc = (size_t)num_heads * nt * nt * 256;
   }
-  size_t extra = 0;
-#ifdef HVK_KL_STAMP
-  extra = HVK_KL_STAMP_U64 * 2;  // diagnostic stamps after the accumulators
-#endif
-  return (acc + (size_t)num_heads * 33 + extra) * sizeof(float);
+  return (acc + (size_t)num_heads * 33) * sizeof(float);
 }
 
 int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
@@ -718,14 +714,8 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
   a.lse = lse;
   a.bias = bias_table;
   a.scale = scale;
-  size_t extra = 0;
-#ifdef HVK_KL_STAMP
-  extra = HVK_KL_STAMP_U64 * 2;
-  a.stamp = reinterpret_cast<unsigned long long*>(
-      workspace + hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) - extra);
-#endif
   const size_t ws_acc = hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) -
-                        (size_t)num_heads * 33 - extra;
+                        (size_t)num_heads * 33;
   a.dbias_acc = workspace;
   a.dscale_acc = workspace + ws_acc;
   a.dqb_acc = a.dscale_acc + num_heads;
@@ -735,8 +725,7 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (hvk_wmsa::large_window(window))
     return hvk_wmsa::large_bwd(a, window, dbias_table, dscale, dq_bias, st);
-  // the forward's row constants given: key-on-lane kernel (wmsa_bwd.hip); else recompute them
-  if (lse) return hvk_wmsa::kl_bwd(a, window, dbias_table, dscale, dq_bias, st);
+  // windows <= 8 always recompute the row constants (exact delta = sum P dP); out / lse unused
   // fill all 256 CUs: 256 / nH chunks, not rounded down to a multiple of 8 (at 12 and 24 heads
   // the rounding left 64 CUs idle), the (chunk, head) items dealt to the XCDs in runs of at
   // most 32 (one resident workgroup per CU of each XCD)

@@ -73,18 +73,14 @@ struct FwdArgs {
   const float* bias;         // [nH, R*R]   16*sigmoid(cpb)
   const float* scale;        // [nH]        exp(clamp(logit_scale))
   float* lse;                // [T, nH] or null: per query, log2 of the softmax denominator of the
-                             // log2e-scaled logits (the backward's row constant, wmsa_bwd.hip)
+                             // log2e-scaled logits (the large-window backward's row constant)
   WmsaGeom g;
 };
 
-#ifdef HVK_KL_STAMP
-// [workgroup < 1024][wave 2][window < 4][phase 8]
-#define HVK_KL_STAMP_U64 (1024 * 2 * 4 * 8)
-#endif
 struct BwdArgs {
   const hvk_bf16* qkv;       // [T, 3C]  x Wqkv^T + (q_bias, 0, 0)
   const hvk_bf16* dout;      // [T, C]   gradient of the attention core output
-  const hvk_bf16* out;       // [T, C]   the forward's output O (key-on-lane kernel: delta = dO . O)
+  const hvk_bf16* out;       // [T, C]   the forward's output O (large windows: delta = dO . O)
   const float* lse;          // [T, nH]  the forward's row constants L2 (FwdArgs::lse), or null
   hvk_bf16* dqkv;            // [T, 3C]
   const float* bias;         // [nH, R*R]
@@ -95,9 +91,6 @@ struct BwdArgs {
   float* dscale_acc;         // [nH]
   float* dqb_acc;            // [C]   column sums of dq (q_bias gradient)
   WmsaGeom g;
-#ifdef HVK_KL_STAMP
-  unsigned long long* stamp;  // diagnostic build: per-phase s_memtime of the key-on-lane kernel
-#endif
 };
 
 // Persistent grid: n_heads * n_chunks <= `capacity` resident workgroups (no tail round),
@@ -133,11 +126,6 @@ int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, floa
 // windows <= 8, forward (wmsa_ring.hip): one persistent workgroup per (window chunk, head
 // group), window slabs staged by LDS-DMA
 int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);
-
-// windows <= 8, backward from the forward's row constants (wmsa_bwd.hip): key on the lane,
-// two 4-wave workgroups per CU; dbias_acc floats it needs; launch (main + finalize)
-size_t kl_acc_floats(int num_heads, int win);
-int kl_bwd(BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias, hipStream_t st);
 
 // finalize helper: per head block, write dscale / dq_bias from the workspace and zero it
 __device__ __forceinline__ void finalize_scale_qb(float* dscale_acc, float* dqb_acc, float* dscale,

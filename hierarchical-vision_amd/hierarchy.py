@@ -341,6 +341,28 @@ class FineGrainedAccuracy(_SumMetric):
         self.den += tgt.numel() / self.topk
 
 
+class Accuracy(_SumMetric):
+    """torchmetrics.Accuracy(task="multiclass", num_classes, top_k) with its default micro
+    average, as models.py:87-97 builds it: a sample counts when its target is among the top_k
+    logits.  Hard taxonomy targets [B, tiers] (the HXE variant's) score the leaf column."""
+
+    def __init__(self, num_classes, top_k=1):
+        super().__init__()
+        if top_k > num_classes:
+            raise ValueError(f"top_k ({top_k}) > num_classes ({num_classes})")
+        self.num_classes = num_classes
+        self.top_k = top_k
+
+    def update(self, preds, targets):
+        if targets.dtype.is_floating_point:
+            raise ValueError("Accuracy takes integer class targets")
+        if targets.ndim == 2:
+            targets = targets[:, -1]
+        top = preds.topk(self.top_k, dim=1, largest=True, sorted=True)[1]
+        self.num += (top == targets.view(-1, 1)).any(dim=1).sum()
+        self.den += targets.numel()
+
+
 class TreeDistance(_SumMetric):
     """Mean tree distance of the top-1 prediction (hierarchy.py:126-154)."""
 
@@ -365,6 +387,8 @@ class CrossEntropyMetric(_SumMetric):
     """Running mean cross-entropy (composer.metrics.CrossEntropy semantics)."""
 
     def update(self, preds, targets):
+        if not targets.dtype.is_floating_point and targets.ndim == 2:
+            targets = targets[:, -1]  # HXE: [B, tiers] taxonomy targets, the leaf column
         b = preds.shape[0]
         self.num += soft_cross_entropy(preds, targets).detach().double() * b
         self.den += b

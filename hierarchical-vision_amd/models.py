@@ -137,19 +137,30 @@ def build_composer_model(config, dataset_info: DatasetInfo, **model_kwargs):
         num_classes = tax.num_leaves
     model = build_model(config, num_classes, **model_kwargs)
 
+    # metrics (models.py:61-101): the same dict keys per variant; "hxe" scores its leaf
+    # logits as the flat variant does
     if variant == "multitask":
-        train_metrics = {"cross-entropy": hierarchy.FineGrainedCrossEntropy(),
-                         "acc@1": hierarchy.FineGrainedAccuracy(topk=1),
-                         "acc@5": hierarchy.FineGrainedAccuracy(topk=5)}
-        val_metrics = {"cross-entropy": hierarchy.FineGrainedCrossEntropy(),
-                       "acc@1": hierarchy.FineGrainedAccuracy(topk=1),
-                       "acc@5": hierarchy.FineGrainedAccuracy(topk=5)}
-        if dataset_info.tree_dists is not None:
+        def fine_grained():
+            return {"cross-entropy": hierarchy.FineGrainedCrossEntropy(),
+                    "acc@1": hierarchy.FineGrainedAccuracy(topk=1),
+                    "acc@5": hierarchy.FineGrainedAccuracy(topk=5)}
+        train_metrics = fine_grained()
+        val_metrics = fine_grained()
+        val_metrics["tree-dist"] = hierarchy.FineGrainedTreeDistance(dataset_info.tree_dists)
+        if not config.is_train:
+            train_metrics["tree-dist"] = hierarchy.FineGrainedTreeDistance(dataset_info.tree_dists)
             val_metrics["tree-dist"] = hierarchy.FineGrainedTreeDistance(dataset_info.tree_dists)
     else:
-        train_metrics = {"cross-entropy": hierarchy.CrossEntropyMetric()}
-        val_metrics = {"cross-entropy": hierarchy.CrossEntropyMetric()}
-        if dataset_info.tree_dists is not None and not config.is_train:
+        assert isinstance(num_classes, int)
+
+        def flat():
+            return {"cross-entropy": hierarchy.CrossEntropyMetric(),
+                    "acc@1": hierarchy.Accuracy(num_classes=num_classes),
+                    "acc@5": hierarchy.Accuracy(num_classes=num_classes, top_k=5)}
+        train_metrics = flat()
+        val_metrics = flat()
+        if not config.is_train:
+            train_metrics["tree-dist"] = hierarchy.TreeDistance(dataset_info.tree_dists)
             val_metrics["tree-dist"] = hierarchy.TreeDistance(dataset_info.tree_dists)
 
     if variant == "hxe":

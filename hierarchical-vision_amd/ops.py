@@ -363,7 +363,6 @@ def _wmsa_workspace(device, nbytes):
     return ws
 
 
-_WMSA_KL = os.environ.get("HVK_WMSA_BWD_KL", "0") == "1"  # 1: key-on-lane backward (probe)
 # windows 12 / 16 / 24: the forward keeps the row constants and the backward skips its
 # row-statistics pass (0: recompute them, A/B runs)
 _WMSA_LARGE_LSE = os.environ.get("HVK_WMSA_LARGE_LSE", "1") != "0"
@@ -377,7 +376,7 @@ class WindowAttentionCore(torch.autograd.Function):
     swinv2.py:399-412 + 221-261 + 420-429 (see include/hvk.h).  `q_bias` is taken only to
     route its gradient: d loss / d q_bias = column sums of dq, produced by the backward
     kernel (the qkv GEMM gets the bias detached, so no separate reduction runs).  For windows
-    12 / 16 / 24 (and <= 8 with HVK_WMSA_BWD_KL=1) the forward also keeps each query's softmax
+    12 / 16 / 24 the forward also keeps each query's softmax
     row constant (4 B per token and head) and the backward takes it with the output (kept
     anyway as proj's saved input) instead of recomputing the row statistics."""
 
@@ -391,7 +390,7 @@ class WindowAttentionCore(torch.autograd.Function):
         bias_table = _f32(bias_table)
         scale = _f32(scale)
         out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
-        keep = (_WMSA_KL and window <= 8) or (_WMSA_LARGE_LSE and window > 8)
+        keep = _WMSA_LARGE_LSE and window > 8
         lse = torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32) if keep else None
         call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(lse), ptr(bias_table), ptr(scale), B, H, W, C,
              num_heads, window, shift, stream())

@@ -55,7 +55,7 @@ class DecoupledSGDW(torch.optim.Optimizer):
         """The fused step can apply an EMA over exactly these parameters when every one of them
         is in a param group (the trainer asks before handing the EMA over)."""
         mine = {id(p) for g in self.param_groups for p in g["params"]}
-        return self._fused_eligible() and all(id(p) in mine for p in params)
+        return self._fused_eligible() and mine == {id(p) for p in params}
 
     def _fused_eligible(self):
         if os.environ.get("HVK_FUSED_OPTIM", "1") == "0":  # A/B runs: the foreach path
@@ -141,7 +141,9 @@ class DecoupledSGDW(torch.optim.Optimizer):
         lr = (ctypes.c_float * 4)(*lr_v)
         decay = (ctypes.c_float * 4)(*decay_v)
         hyper = None
-        if self.device_hyper and self._hyper is not None:
+        # the device array only inside a capture (replay() refreshes it); an eager step takes
+        # the current lr / decay as arguments, so a schedule change is never missed
+        if self.device_hyper and self._hyper is not None and torch.cuda.is_current_stream_capturing():
             hyper = _lib.ptr(self._hyper)
             self.hyper_used = True
         lib = _lib.load()

@@ -66,9 +66,9 @@ int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
 /* dout: bf16 [B*H*W, C] (grad of `out`); out, lse: the forward's output and row constants,
  * or both NULL (every window: the softmax row statistics are recomputed from q, k).  Given
- * them, windows <= 8 run the key-on-lane kernel (delta = rowsum(dout o out)), windows
- * 12/16/24 skip the row-statistics pass (delta from dout o out, corrected by the exact dS
- * and P row sums for dq, dk, dv and dscale);
+ * them, windows 12/16/24 skip the row-statistics pass (delta from dout o out, corrected by the
+ * exact dS and P row sums for dq, dk, dv and dscale); windows <= 8 ignore them and recompute
+ * (exact delta = rowsum(P o dP));
  * dqkv: bf16 [B*H*W, 3C] (fully overwritten);
  * dq_bias: f32 [C] (overwritten: column sums of the q part of dqkv = d loss / d q_bias,
  * replacing the qkv bias-gradient reduction) or NULL; dbias_table: f32 [num_heads,

@@ -92,7 +92,7 @@ class _OracleSwin(torch.nn.Module):
                                         t.tier_base, self.lam)
 
 
-def _train(rank, world, port, out, clip, steps=2):
+def _train(rank, world, port, out, clip, steps=2, clip_type="norm"):
     from hvamd.algorithmic import EMA, GradientClipping
     from hvamd.hierarchy import Taxonomy
     from hvamd.optim import DecoupledSGDW, set_weight_decay
@@ -105,7 +105,7 @@ def _train(rank, world, port, out, clip, steps=2):
     model = _OracleSwin(tax)
     opt = DecoupledSGDW(set_weight_decay(model), lr=0.05, momentum=0.9, weight_decay=5e-4)
     ema = EMA(half_life="4ba", update_interval="1ba")
-    trainer = Trainer(model, opt, [GradientClipping("norm", clip), ema], bucket_mb=0.05)
+    trainer = Trainer(model, opt, [GradientClipping(clip_type, clip), ema], bucket_mb=0.05)
     if world > 1:
         assert len(trainer.buckets.buckets) > 2  # several all-reduces in flight in the backward
     g = torch.Generator().manual_seed(7)
@@ -121,17 +121,18 @@ def _train(rank, world, port, out, clip, steps=2):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("clip", [0.5, 1e4])  # clipping active / inactive (the mean must matter)
-def test_trainer_world2_equals_single_process_full_batch(clip):
+@pytest.mark.parametrize("clip_type,clip", [("norm", 0.5), ("norm", 1e4), ("value", 2e-3)])
+def test_trainer_world2_equals_single_process_full_batch(clip_type, clip):
     """The real Trainer (bucketed hook-driven all-reduce with the 1/world mean handed to
     DecoupledSGDW, GradientClipping handed over as well, EMA every batch) on two gloo ranks
     with half the batch each: parameters and EMA weights after two steps equal one process
-    stepping on the whole batch (main.py:44-48 batch split, :104-124 DDP)."""
+    stepping on the whole batch (main.py:44-48 batch split, :104-124 DDP).  Value clipping
+    is not handed over: it must see the mean, not the bucket sums (threshold active here)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_train, args=(2, _free_port(), out, clip), nprocs=2, join=True)
+    mp.spawn(_train, args=(2, _free_port(), out, clip, 2, clip_type), nprocs=2, join=True)
     single = {}
-    _train(0, 1, 0, single, clip)
+    _train(0, 1, 0, single, clip, 2, clip_type)
     for r in range(2):
         for a, b in zip(out[r][0] + out[r][1], single[0][0] + single[0][1]):
             assert torch.allclose(torch.from_numpy(a), torch.from_numpy(b), rtol=1e-4, atol=1e-6), r

@@ -82,3 +82,28 @@ def test_graph_replay_follows_lr_schedule():
     for (na, pa), (nb, pb) in zip(model.named_parameters(), model_b.named_parameters()):
         rel = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
         assert rel < 1e-2, (na, rel)
+
+
+def test_eager_step_after_capture_takes_current_lr():
+    """After capture() the fused update reads lr / decay from a device array only inside the
+    captured graph: an eager step after an lr change (e.g. the warm-up steps of a second
+    capture) must use the new lr, not the value of the last replay's refresh."""
+    tax, model, dev = _setup()
+    model_b = copy.deepcopy(model)
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(4, 3, 56, 56, device=dev, generator=g)
+    y = torch.tensor(tax.leaf_paths[[1, 5, 9, 11]], device=dev)
+    ta, tb = _trainer(model), _trainer(model_b)
+    for _ in range(4):
+        ta.train_step((x, y))
+    tb.capture((x, y), warmup=3)
+    tb.replay()
+    torch.cuda.synchronize()
+    for t in (ta, tb):
+        for grp in t.optimizer.param_groups:
+            grp["lr"] = 0.0  # an eager step at lr 0 moves only by weight decay (decay = 1 at lr 0)
+    before = [p.detach().clone() for p in model_b.parameters()]
+    tb.train_step((x, y))
+    torch.cuda.synchronize()
+    for (n, p), b in zip(model_b.named_parameters(), before):
+        assert torch.equal(b, p.detach()), n

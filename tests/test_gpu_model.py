@@ -417,3 +417,56 @@ def test_swinv2t_hxe_train_step_vs_oracle():
     assert len(mine) > 200, len(mine)
     assert not bad, bad
     assert rel(torch.cat(mine), torch.cat(theirs)) < 3e-2
+
+
+def test_activation_checkpointing_matches_plain_step():
+    """use_checkpoint=True (swinv2.py:584-585): every block is recomputed in the backward through
+    the libhvk autograd functions, reusing the step's planned DropPath scales and its cached bf16
+    weight copies.  Loss, input and parameter gradients equal the non-checkpointed step (the only
+    difference allowed: the order of the backward's f32 atomic sums)."""
+    from hvamd.swinv2 import SwinTransformerV2
+    cfg = dict(MINI, drop_path_rate=0.2)  # DropPath active: the recompute must reuse the masks
+    res = {}
+    for ckpt in (False, True):
+        torch.manual_seed(0)
+        net = SwinTransformerV2(num_classes=10, use_checkpoint=ckpt, **cfg)
+        shapes = {k: v.shape for k, v in net.state_dict().items()
+                  if k.endswith(("weight", "bias", "logit_scale")) and "relative" not in k}
+        net.load_state_dict(swinv2_ref.init_params_from_rng(shapes, 7), strict=False)
+        net = net.cuda().train()
+        x = torch.from_numpy(np.random.default_rng(42).standard_normal((4, 3, 56, 56)).astype(np.float32))
+        x = x.cuda().requires_grad_(True)
+        torch.manual_seed(1)  # same DropPath draw in both runs
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = net(x)
+        y.float().square().sum().backward()
+        torch.cuda.synchronize()
+        res[ckpt] = (y.detach().float().cpu(), x.grad.cpu(),
+                     {k: p.grad.float().cpu() for k, p in net.named_parameters()})
+    (y0, gx0, g0), (y1, gx1, g1) = res[False], res[True]
+    assert torch.equal(y0, y1)
+    assert rel(gx1, gx0) < 1e-5
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-4, k
+
+
+def test_feature_only_model_forward_head_pre_logits():
+    """FeatureOnlyModel (models.py:186-205) calls forward_head(forward_features(x), pre_logits=True):
+    the pooled features, equal to forward_features; forward_head without pre_logits is the head."""
+    from hvamd import configs, models
+    net = _model(MINI, 10).eval()
+    x = torch.from_numpy(np.random.default_rng(3).standard_normal((2, 3, 56, 56)).astype(np.float32)).cuda()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        feats = net.forward_features(x)
+        pre = net.forward_head(feats, pre_logits=True)
+        logits = net.forward_head(feats)
+        full = net(x)
+        fo = models.FeatureOnlyModel(net)(x)
+    assert feats.shape == (2, net.num_features)
+    assert torch.equal(pre, feats) and torch.equal(fo, feats)
+    assert torch.equal(logits, full)
+    assert not any(p.requires_grad for p in net.parameters())  # frozen by FeatureOnlyModel
+    cfg = configs.Config()
+    cfg.model.name = "swinv2_tiny_window7_224"
+    cfg.model.variant = "linear-probe"
+    assert isinstance(models.build_model(cfg, 10), models.FeatureOnlyModel)

@@ -166,29 +166,6 @@ def test_wmsa_rejects_unsupported_head_dim():
                                   torch.ones(1, device="cuda"), 7, 7, 1, 7, 0)
 
 
-@pytest.mark.parametrize("B,H,W,nh,win,shift", [(2, 14, 14, 2, 7, 3), (1, 16, 16, 3, 8, 4), (1, 12, 12, 4, 6, 3),
-                                                (2, 8, 8, 2, 4, 2), (2, 7, 7, 24, 7, 0)])
-def test_wmsa_backward_paths_agree(monkeypatch, B, H, W, nh, win, shift):
-    """The key-on-lane backward (forward row constants + delta = dO.O) and the recomputing
-    backward give the same gradients (up to bf16 rounding of their different operand orders)."""
-    import hvamd.ops as ops
-    qkv, tab, scale = _inputs(B, H, W, nh, win, 4)
-    gout = torch.from_numpy(np.random.default_rng(6).standard_normal((B, H * W, 32 * nh)).astype(np.float32))
-    res = {}
-    for kl in (True, False):
-        monkeypatch.setattr(ops, "_WMSA_KL", kl)
-        q = qkv.cuda().bfloat16().requires_grad_(True)
-        t = tab.cuda().requires_grad_(True)
-        s = scale.cuda().requires_grad_(True)
-        qb = torch.zeros(32 * nh, device="cuda", requires_grad=True)
-        ops.window_attention_core(q, t, s, H, W, nh, win, shift, q_bias=qb).backward(gout.cuda().bfloat16())
-        res[kl] = [x.grad.float().cpu() for x in (q, t, s, qb)]
-    for name, a, b in zip(("dqkv", "dbias", "dscale", "dq_bias"), res[True], res[False]):
-        rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
-        assert rel < (3e-2 if name == "dscale" else 1e-2), (name, rel)
-
-
-
 @pytest.mark.parametrize("B,H,W,nh,win,shift", [(1, 24, 24, 2, 12, 6), (1, 48, 48, 2, 24, 12),
                                                 (1, 24, 24, 3, 24, 0), (1, 32, 32, 2, 16, 8)])
 @pytest.mark.parametrize("scale_kind", ["random", "anti100"])

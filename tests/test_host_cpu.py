@@ -186,6 +186,43 @@ def test_composer_model_surface_and_hxe_wiring():
         models.build_composer_model(cfg, models.DatasetInfo(num_classes=12))
 
 
+def test_metric_dicts_match_reference_and_topk_known_answer():
+    """models.py:61-101: the metric keys per variant and is_train, and acc@1 / acc@5 on a
+    hand-made batch (torchmetrics multiclass micro accuracy: target among the top-k)."""
+    from hvamd import configs, hierarchy, models
+    tax = hierarchy.Taxonomy.synthetic((2, 3, 4, 5, 6, 7, 12))
+    dists = torch.zeros(12, 12, dtype=torch.uint8)
+    flat, fg = ["cross-entropy", "acc@1", "acc@5"], ["cross-entropy", "acc@1", "acc@5"]
+    for variant, is_train, train_keys, val_keys in [
+            ("", True, flat, flat), ("", False, flat + ["tree-dist"], flat + ["tree-dist"]),
+            ("hxe", True, flat, flat), ("hxe", False, flat + ["tree-dist"], flat + ["tree-dist"]),
+            ("multitask", True, fg, fg + ["tree-dist"]),
+            ("multitask", False, fg + ["tree-dist"], fg + ["tree-dist"])]:
+        cfg = configs.Config()
+        cfg.model.name = "swinv2_tiny_window7_224"
+        cfg.hierarchy.variant = variant
+        cfg.is_train = is_train
+        nc = tuple(tax.num_classes) if variant == "multitask" else 12
+        m = models.build_composer_model(cfg, models.DatasetInfo(num_classes=nc, tree_dists=dists,
+                                                                taxonomy=tax))
+        assert list(m.get_metrics(is_train=True)) == train_keys, (variant, is_train)
+        assert list(m.get_metrics(is_train=False)) == val_keys, (variant, is_train)
+        assert m.get_metrics(is_train=True)["acc@1"] is not m.get_metrics(is_train=False)["acc@1"]
+    # known answer: 4 samples over 6 classes
+    logits = torch.tensor([[0.0, 5, 4, 3, 2, 1],    # target 1: top-1 hit
+                           [9.0, 0, 1, 2, 3, 4],    # target 5: 2nd -> top-5 hit only
+                           [0.0, 1, 2, 3, 4, 5],    # target 0: rank 6 -> miss both
+                           [1.0, 2, 3, 4, 5, 6]])   # target 1: rank 5 -> top-5 hit
+    tgt = torch.tensor([1, 5, 0, 1])
+    a1, a5 = hierarchy.Accuracy(6), hierarchy.Accuracy(6, top_k=5)
+    a1.update(logits, tgt)
+    a5.update(logits, tgt)
+    assert a1.compute().item() == pytest.approx(0.25)
+    assert a5.compute().item() == pytest.approx(0.75)
+    a5.update(logits, torch.stack([tgt] * 7, dim=1))  # [B, tiers] taxonomy targets: leaf column
+    assert a5.compute().item() == pytest.approx(0.75)
+
+
 def test_optimizer_groups_follow_reference_rule():
     from hvamd import configs, models, optim
     cfg = configs.Config()

@@ -45,34 +45,14 @@ def timeit(fn, iters, kind):
     return t.value / max(n.value, 1)
 
 
-def print_stamps(ws, bwd):
-    """Median cycles per phase over the first windows of the first 1024 workgroups (the
-    diagnostic build's s_memtime stamps at the tail of the workspace)."""
-    n = 1024 * 2 * 4 * 8
-    ws[-2 * n:].zero_()
-    bwd()
-    torch.cuda.synchronize()
-    st = torch.from_numpy(ws[-2 * n:].cpu().numpy().view("int64").reshape(1024, 2, 4, 8))
-    ok = (st[..., :7] > 0).all(-1)
-    d = (st[..., 1:7] - st[..., 0:6]).float()
-    names = ["barrier0", "stage", "barrier1", "key_tiles", "barrier2", "query_tiles"]
-    for wv in range(2):
-        sel = ok[:, wv, 1:]
-        row = [float(d[:, wv, 1:, k][sel].median()) for k in range(6)]
-        loop = (st[:, wv, 2:4, 0] - st[:, wv, 1:3, 0]).float()[ok[:, wv, 1:3]]
-        print(f"    wave {wv}: " + "  ".join(f"{nm} {v:6.0f}" for nm, v in zip(names, row)) +
-              f"  | window {float(loop.median()):6.0f}")
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default=None, help="alternative libhvk build (tools/probe)")
     ap.add_argument("--stage", type=int, default=None, help="only this stage (0-3)")
     ap.add_argument("--only", choices=["fwd", "bwd"], default=None)
-    ap.add_argument("--kl", type=int, default=1, help="1: forward keeps row constants, key-on-lane backward")
-    ap.add_argument("--stamps", action="store_true",
-                    help="diagnostic build (-DHVK_KL_STAMP): per-phase cycles of the key-on-lane backward")
+    ap.add_argument("--recompute", action="store_true",
+                    help="large windows: backward recomputes the row statistics (no forward row constants)")
     ap.add_argument("--b384", action="store_true", help="SwinV2-B 384 w24 stage shapes (config 5)")
     args = ap.parse_args()
     from hvamd import _lib
@@ -99,7 +79,8 @@ def main():
         P = _lib.ptr
         st = _lib.stream
 
-        lse = torch.empty(T, nh, device="cuda") if args.kl else None
+        keep = win > 8 and not args.recompute  # as ops.WindowAttentionCore
+        lse = torch.empty(T, nh, device="cuda") if keep else None
 
         def fwd():
             _lib.call("hvk_wmsa_fwd", P(qkv), P(out), P(lse), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
@@ -107,13 +88,11 @@ def main():
         fwd()  # out / lse for the backward
 
         def bwd():
-            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(out) if args.kl else None, P(lse), P(dqkv), P(dqb),
+            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(out) if keep else None, P(lse), P(dqkv), P(dqb),
                       P(tab), P(scale), P(dtab), P(dsc), P(ws), wsb, B, H, W, C, nh, win, sh, st())
 
         tf = timeit(fwd, args.iters, 0) if args.only != "bwd" else float("nan")
         tb = timeit(bwd, args.iters, 1) if args.only != "fwd" else float("nan")
-        if args.stamps:
-            print_stamps(ws, bwd)
         bf, bb = 8 * T * C, 16 * T * C
         tot_f += tf * nblk
         tot_b += tb * nblk

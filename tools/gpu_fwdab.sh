@@ -5,5 +5,5 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/fwdab_tests.log; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do for v in ${KLV:-base new}; do
   echo "== $v"
-  HVK_LIB_PATH=$PWD/abl/$v.so timeout -k 10 300 python tools/bench_wmsa.py --only fwd --kl 0 || exit 1
+  HVK_LIB_PATH=$PWD/abl/$v.so timeout -k 10 300 python tools/bench_wmsa.py --only fwd || exit 1
 done; done

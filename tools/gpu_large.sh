@@ -9,5 +9,5 @@ tail -4 gpurun_out/large_tests.log
 fi
 for v in ${KLV:-}; do
   echo "== $v"
-  HVK_LIB_PATH=$PWD/abl/$v.so timeout -k 10 300 python tools/bench_wmsa.py --b384 --kl 0 --iters 3 ${BW_ARGS:-} || exit 1
+  HVK_LIB_PATH=$PWD/abl/$v.so timeout -k 10 300 python tools/bench_wmsa.py --b384 --iters 3 ${BW_ARGS:-} || exit 1
 done
