@@ -1,6 +1,7 @@
 // Shared pieces of the W-MSA kernels (wmsa.hip: windows <= 8, wmsa_large.hip: 12/16/24).
 #pragma once
 #include "hvk_common.h"
+#include <type_traits>
 
 namespace hvk_wmsa {
 
@@ -62,6 +63,10 @@ __device__ __forceinline__ int fm16(int row, int u) {  // byte offset of 16-B un
 }
 __device__ __forceinline__ int fm8(int row, int col8) {  // byte offset of 8-B unit col8
   return fm16(row, col8 >> 1) + ((col8 & 1) << 3);
+}
+// LDS byte address of a pointer into dynamic shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
 __device__ __forceinline__ uint4 lds16(const char* img, int off) {
   return *reinterpret_cast<const uint4*>(img + off);

@@ -3,33 +3,24 @@
 //
 // Same semantics and token layout as wmsa.hip (reference: swinv2.py:221-261 + roll/partition
 // 399-412 / reverse 420-429), but a window no longer fits one wave's registers
-// (N = 144 ... 576 tokens), so one WORKGROUP owns one (window, head):
-//   forward   K^ and V of the window are staged once in LDS; every wave streams its query
-//             tiles against all keys in 32-key chunks with an online softmax (flash form);
-//   backward  phase 1 (query on the lane, K^ / V in LDS): row max / sum / delta, then dS,
-//             dQ, the CPB-bias and logit-scale gradients; phase 2 (key on the lane, Q^ / dO
-//             restaged in the same LDS): dK, dV.  Nothing is saved by the forward.
-// The CPB table stays compact ((2w-1)^2 floats per head, log2e-scaled) and is looked up per
-// score element: index = bq(query) - bk(key), bq = (qh+w-1)(2w-1) + qw+w-1, bk = kh(2w-1)+kw.
-// The bias gradient is binned with LDS float atomics and flushed once per workgroup.
+// (N = 144 ... 576 tokens), so a WORKGROUP owns a (window, head) at a time; workgroups are
+// persistent, one head each over a run of windows (XCD-aware: the heads of a window run share
+// one L2):
+//   forward   k^ and v of the window sit in LDS (the next window's streamed in by LDS-DMA
+//             meanwhile); every wave runs its query tiles against all keys in 32-key chunks;
+//   backward  phase 1 (query on the lane, k^ / v in LDS): dS, dQ, the exact delta;
+//             phase 2 (key on the lane, q^ / dO in LDS): dK, dV, the CPB-table and
+//             logit-scale gradients.  The forward's row constants (LSE) spare the backward
+//             its row-statistics pass.
+// The CPB table stays compact ((2w-1)^2 floats per head, log2e-scaled, mirrored) and enters the
+// score MFMAs as their C operand: index = bq(query) - bk(key), bq = (qh+w-1)(2w-1) + qw+w-1,
+// bk = kh(2w-1) + kw.
 //
 // LDS images are [rows][32] bf16 in "fragment-major" order: the 16-B unit (row, u) of a
 // 16-row tile sits at slot 16u + (row%16 ^ 12*(u&1)), so the natural MFMA operand read
 // (ds_read_b128, lane = row%16 + 16u) and the transposed read (ds_read_b64_tr_b16) are both
 // bank-conflict free (checked with the LDS bank model of MI355X_MICROARCH.md).
 #include "wmsa_common.h"
-
-// experiment builds (not the product): 1 no CPB-gradient accumulation, 3 no edge masks,
-// 4 no phase 2, 5 no phase-1 loop B, 6 no phase-1 loop A
-#ifndef HVK_LARGE_PROBE
-#define HVK_LARGE_PROBE 0
-#endif
-#ifndef HVK_LARGE_FWAVES24  // forward waves per workgroup at w24 (9 / 12 / 16: 19.3 / 18.3 / 16.9 ms per SwinV2-B 384 step)
-#define HVK_LARGE_FWAVES24 16
-#endif
-#ifndef HVK_LARGE_BINS
-#define HVK_LARGE_BINS 1
-#endif
 
 namespace hvk_wmsa {
 namespace {
@@ -42,18 +33,8 @@ struct LCfg {
   static constexpr int ROWS = 32 * NC;         // padded rows of an LDS image
   static constexpr int R = 2 * WIN - 1;
   static constexpr int RR = R * R;             // CPB table entries per head
-  static constexpr int WAVES = WIN == 16 ? 8 : (WIN == 24 ? HVK_LARGE_FWAVES24 : 9);
-  static constexpr int THREADS = 64 * WAVES;
-  static constexpr int QB = (NT % (2 * WAVES) == 0) ? 2 : 1;  // query tiles per forward pass
   static constexpr int IMG = ROWS * 64;        // bytes per image
-  static_assert(NT % WAVES == 0 || QB == 1, "tile split");
-  static_assert(N == 16 * NT, "strided query tiles cover the window exactly");
-  // backward: BWAVES waves, each with a private copy of the CPB-gradient bins (plain LDS
-  // read-add-write, no float atomics) when HVK_LARGE_BINS; 8 waves at w24 so that the 8
-  // copies fit beside the two images
-  static constexpr int BWAVES = HVK_LARGE_BINS ? 8 : WAVES;
-  static constexpr int BTHREADS = 64 * BWAVES;
-  static constexpr int RRP = (RR + 3) / 4 * 4;  // bins per copy (16-B aligned)
+  static_assert(N == 16 * NT, "strided tiles cover the window exactly");
   // mirrored CPB table: entry j = RR - 1 - (bq - bk), so the 4 consecutive keys 4g .. 4g+3 of
   // a lane (one window row: 4 | WIN) read 4 ascending floats (two ds_read2_b32) straight into
   // the MFMA C operand; padding keys (w12's last chunk) index past RR into zeros
@@ -70,615 +51,859 @@ __device__ __forceinline__ uint4 tr_frag(const char* img, int c, int dt, int li,
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
-template <int WIN>
-struct PosInfo {  // window-local geometry of one token position
-  int b;          // bias-index base: bq for a query, bk for a key
-  bool r, c;      // in the last shift band of its row / column
-};
-template <int WIN>
-__device__ __forceinline__ PosInfo<WIN> query_info(int pos, int lim) {
-  const int ph = pos / WIN, pw = pos - ph * WIN;
-  return {(ph + WIN - 1) * LCfg<WIN>::R + pw + WIN - 1, ph >= lim, pw >= lim};
-}
-template <int WIN>
-__device__ __forceinline__ PosInfo<WIN> key_info(int pos, int lim) {
-  const int ph = pos / WIN, pw = pos - ph * WIN;
-  return {ph * LCfg<WIN>::R + pw, ph >= lim, pw >= lim};
-}
 // ------------------------------------------------------------------------------ forward
-// Per query tile (query on the lane), keys in 32-key chunks: S' = K^ (scale log2e Q^)^T +
-// (log2e bias - M_h) with the mirrored bias table as the MFMA C operand, M_h = scale log2e +
-// max bias the head bound of every logit (as the ring kernel, wmsa_ring.hip), so the fast path
-// exponentiates S' directly -- no running max, no rescaling -- and checks the row sums at the
-// end: a tile where any row sum fell below 2^-100 (a row far below the head bound, scale ~100)
-// is recomputed with the true running max (the reference's softmax, swinv2.py:256).
-template <int WIN, bool LSE>
-__global__ __launch_bounds__(LCfg<WIN>::THREADS, 1) void wmsa_fwd_large_kernel(FwdArgs a) {
+// Persistent workgroups, one head each, walking a run of windows (so the head's CPB table and
+// bound are set up once), K and V of the NEXT window streamed into a second LDS buffer by
+// LDS-DMA while this window computes.  Per window: wait for its DMA, normalise k^ in place
+// (one pass over the image), barrier, then every wave runs its QT query tiles (positions
+// 16 (wave + WAVES j) + li: whole window rows apart, so their bias indices differ by a
+// compile-time step) jointly over all 32-key chunks, reading each K / V fragment once for the
+// QT tiles.  S' = K^ (scale log2e Q^)^T + (log2e bias - M_h) comes from one MFMA with the
+// mirrored CPB table as its C operand, M_h = scale log2e + max bias the head bound of every
+// logit, so P = exp2(S') needs no running max; the row sums come from a ones-vector MFMA over
+// the same bf16 P that multiplies V.  A tile whose row sum fell below 2^-100 (a row far below
+// the head bound, scale ~100) is recomputed with the true running max (the reference's
+// softmax, swinv2.py:256).  Interior windows and unshifted blocks run a mask-free copy of the
+// loop; edge windows of shifted blocks add the -100 mask (swinv2.py:249-254), per 4-key group
+// when 4 | (window - shift) (a lane's 4 keys share their region), else per element.
+template <int WIN>
+struct FCfg {
   using K = LCfg<WIN>;
+  static constexpr int WAVES = WIN == 24 ? 12 : (WIN == 16 ? 8 : 3);
+  static constexpr int OCC = WIN == 24 ? 1 : (WIN == 16 ? 2 : 3);  // workgroups per CU (LDS)
+  static constexpr int QT = K::NT / WAVES;                          // query tiles per wave
+  static_assert(K::NT % WAVES == 0, "whole query tiles per wave");
+  static constexpr int DQ = 16 * WAVES;                             // position step between them
+  static_assert(DQ % WIN == 0, "a wave's query tiles are whole window rows apart");
+  static constexpr int DR = (DQ / WIN) * K::R;                      // bias-index step between them
+  static constexpr int BLK = K::ROWS / 16;                          // 1-KB DMA blocks per image
+  static constexpr int BUF = 2 * K::IMG;                            // k^ and v of one window
+  static constexpr size_t LDS = 2 * (size_t)BUF + (size_t)K::TABM * 4 + 64;
+  static constexpr int MINW = (OCC * WAVES) / 4 > 0 ? (OCC * WAVES) / 4 : 1;  // waves per SIMD
+  // chunks per period of whole window rows (the main loop's unroll), 0: none divides NC
+  static constexpr int PER = (32 * 3) % WIN == 0 && K::NC % 3 == 0 ? 3 : (32 % WIN == 0 ? 1 : 0);
+};
+
+// LDS-DMA of 16 B per lane from base + voff into LDS m0 + 16 lane, issued from inline asm: the
+// compiler's wait-count pass does not see it, so it never drains it with the vmcnt(0) it puts
+// in front of LDS reads while one of its own LDS-DMAs is pending.  The kernel waits for it with
+// an explicit s_waitcnt before the barrier that publishes the buffer.
+__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t m0) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(m0), "v"(voff), "s"(base) : "memory");
+}
+// barrier without the vmcnt(0) a __syncthreads() fence adds (the next window's DMA and
+// query loads stay in flight); LDS writes before it are waited for
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int WIN, bool LSE>
+__global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_fwd_large_kernel(FwdArgs a) {
+  using K = LCfg<WIN>;
+  using F = FCfg<WIN>;
+  constexpr int QT = F::QT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WmsaGeom& g = a.g;
-  int w, h;
-  hvk_decode_chunk_head(blockIdx.x, g.nH, w, h);
-  if (w >= g.n_windows) return;
-  char* kimg = smem;
-  char* vimg = smem + K::IMG;
-  float* mtab = reinterpret_cast<float*>(smem + 2 * K::IMG);
+  int chunk, h;
+  if (!decode_item(g, blockIdx.x, chunk, h)) return;
+  const int w0 = (int)((long long)chunk * g.n_windows / g.n_chunks);
+  const int w1 = (int)((long long)(chunk + 1) * g.n_windows / g.n_chunks);
+  if (w0 >= w1) return;
+  float* mtab = reinterpret_cast<float*>(smem + 2 * F::BUF);
   float* red = mtab + K::TABM;  // [WAVES] max-bias partials
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
-  const int C = g.C, C3 = 3 * C;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int li = lane & 15, gq = lane >> 4;
+  const int C = g.C;
   const int per_img = g.nWh * g.nWw;
-  const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
   const float sc2 = a.scale[h] * HVK_LOG2E;
+  const uint32_t sbase = lds_addr(smem);
+  const char* qkv = reinterpret_cast<const char*>(a.qkv);
+  const unsigned RB = 6u * C;  // bytes per qkv token row
+  const size_t IMGB = (size_t)g.H * g.W * RB;
 
+  // LDS-DMA of window (b, wh, ww) into the buffer at LDS byte address buf: instruction j fills
+  // 1 KB of the fm16 image (16 rows x 4 16-B columns): lane L loads row 16 blk + drow, 16-B
+  // column L / 16 (the inverse of fm16).  Padding rows (w12) load the window's first token:
+  // finite values that the -inf key mask / P = 0 leave without effect.
+  const int drow = (lane & 15) ^ (((lane >> 4) & 1) * 12);
+  const unsigned lane_col = (unsigned)(h * 64 + (lane >> 4) * 16);
+  auto issue = [&](int b, int wh, int ww, uint32_t buf) {
+    const char* img = qkv + (size_t)b * IMGB;
+    const int y0 = wh * WIN + g.shift, x0 = ww * WIN + g.shift;
+    for (int j = wave; j < 2 * F::BLK; j += F::WAVES) {
+      const int part = j >= F::BLK ? 1 : 0;
+      const int blk = j - part * F::BLK;
+      int pos = 16 * blk + drow;
+      if (K::ROWS != K::N) pos = pos < K::N ? pos : 0;
+      int y = y0 + pos / WIN, x = x0 + pos % WIN;
+      if (y >= g.H) y -= g.H;
+      if (x >= g.W) x -= g.W;
+      const unsigned voff = (unsigned)(y * g.W + x) * RB + (unsigned)((1 + part) * 2 * C) + lane_col;
+      dma16(img, voff, buf + (uint32_t)(part * K::IMG + blk * 1024));
+    }
+  };
+  // this wave's query tiles: positions 16 (wave + WAVES j) + li (bias index step DR per tile)
+  const int qp0 = 16 * wave + li, qy0 = qp0 / WIN, qx = qp0 % WIN;
+  const int tq0 = K::RR - 1 - ((qy0 + WIN - 1) * K::R + qx + WIN - 1);  // mirrored entry base
+  int qrow[QT];
+  uint4 qn[QT];  // raw q of the next window (in flight under this window's math)
+  auto load_q = [&](int b, int wh, int ww) {
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+      qrow[j] = window_token_row(g, b, wh, ww, WIN, qp0 + F::DQ * j);
+      qn[j] = hvk_ld16(a.qkv + (size_t)qrow[j] * (3 * C) + h * 32 + 8 * gq);
+    }
+  };
+
+  // the head's bound and mirrored table, once per workgroup (every window is head h)
   const float* bsrc = a.bias + (size_t)h * K::RR;
   float mb = -INFINITY;
-  for (int e = threadIdx.x; e < K::RR; e += K::THREADS) mb = fmaxf(mb, bsrc[e]);
+  for (int e = threadIdx.x; e < K::RR; e += 64 * F::WAVES) mb = fmaxf(mb, bsrc[e]);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
   if (lane == 0) red[wave] = mb;
-  // stage k^ (natural fragments) and v (head_dim permuted for 16-B output stores, as in
-  // wmsa.hip: col 16dt + 4g + r <-> d = 8g + 4dt + r)
-  for (int t = wave; t < 2 * K::NC; t += K::WAVES) {
-    const int pos = 16 * t + li;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = kv;
-    if (pos < K::N) {
-      const hvk_bf16* p = a.qkv + (size_t)window_token_row(g, b, wh, ww, WIN, pos) * C3 + h * 32 + 8 * gq;
-      kv = hvk_ld16(p + C);
-      vv = hvk_ld16(p + 2 * C);
-    }
-    float rn;
-    kv = l2_normalize(kv, rn);  // a zero (padding) row stays zero
-    *reinterpret_cast<uint4*>(kimg + fm16(pos, gq)) = kv;
-    *reinterpret_cast<uint2*>(vimg + fm8(pos, gq)) = make_uint2(vv.x, vv.y);
-    *reinterpret_cast<uint2*>(vimg + fm8(pos, 4 + gq)) = make_uint2(vv.z, vv.w);
-  }
+  int cb = w0 / per_img, cwh = (w0 % per_img) / g.nWw, cww = w0 % g.nWw;
+  issue(cb, cwh, cww, sbase);
+  load_q(cb, cwh, cww);
   __syncthreads();
   float Mh = red[0];
 #pragma unroll
-  for (int i = 1; i < K::WAVES; ++i) Mh = fmaxf(Mh, red[i]);
+  for (int i = 1; i < F::WAVES; ++i) Mh = fmaxf(Mh, red[i]);
   Mh = Mh * HVK_LOG2E + sc2;
-  for (int e = threadIdx.x; e < K::TABM; e += K::THREADS) {
+  for (int e = threadIdx.x; e < K::TABM; e += 64 * F::WAVES) {
     const int i = K::RR - 1 - e;
     mtab[e] = i >= 0 ? bsrc[i] * HVK_LOG2E - Mh : 0.f;
   }
-  __syncthreads();
-
+  // A operand of the row-sum MFMA: 1.0 for real keys of chunk c in k-slot order
+  // (slot 8 gq + j <-> key 32c + 4gq + j for j < 4, 32c + 16 + 4gq + j - 4 for j >= 4)
+  auto ones = [&](int c) {
+    uint32_t wv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * jj + e;
+        const int p = 32 * c + (j < 4 ? 4 * gq + j : 16 + 4 * gq + j - 4);
+        if (p < K::N) v |= 0x3F80u << (16 * e);
+      }
+      wv[jj] = v;
+    }
+    return make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  };
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
-  const bool edge = g.shift && (wh == g.nWh - 1 || ww == g.nWw - 1);
-  const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+  constexpr int NST = QT * (LSE ? 2 : 1);  // global stores per window per wave (out, lse)
 
-  for (int t0 = wave * K::QB; t0 < K::NT; t0 += K::WAVES * K::QB) {
-    uint4 qf[K::QB];
-    int qrow[K::QB];
-    PosInfo<WIN> qi[K::QB];
-    hvk_f32x4 o[K::QB][2];
-    float l[K::QB];
-#pragma unroll
-    for (int j = 0; j < K::QB; ++j) {
-      const int pos = 16 * (t0 + j) + li;
-      qrow[j] = window_token_row(g, b, wh, ww, WIN, pos);
-      qf[j] = hvk_ld16(a.qkv + (size_t)qrow[j] * C3 + h * 32 + 8 * gq);
+  for (int w = w0, cur = 0; w < w1; ++w, cur ^= 1) {
+    // this window's DMA and query loads have landed (younger: the previous window's stores)
+    if (w == w0)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    lds_barrier();  // every wave's DMA landed; the other buffer is free (previous window done)
+    char* kimg = smem + cur * F::BUF;
+    char* vimg = kimg + K::IMG;
+    for (int blk = wave; blk < F::BLK; blk += F::WAVES) {  // k^ in place
+      const int off = fm16(16 * blk + li, gq);
       float rn;
-      qf[j] = l2_normalize(qf[j], rn, sc2);  // q^ * scale * log2e
-      qi[j] = query_info<WIN>(pos, lim);
+      *reinterpret_cast<uint4*>(kimg + off) = l2_normalize(lds16(kimg, off), rn);
     }
-    // S' of (key chunk c, half t, query tile j), masked; padding keys -inf
-    auto scores = [&](int c, int t, int j, const uint4& kf) {
-      const int kp = 32 * c + 16 * t + 4 * gq;  // this lane's 4 keys kp .. kp + 3 (one row)
-      const int ky = kp / WIN, kx = kp - ky * WIN;
-      const float* tp = mtab + (K::RR - 1 - qi[j].b + ky * K::R + kx);
+    // this window's queries (normalised, times scale log2e): the loads are complete
+    uint4 qf[QT];
+    int rows[QT];
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+      hvk_u32x4 v = __builtin_bit_cast(hvk_u32x4, qn[j]);
+      asm volatile("" : "+v"(v));  // a fresh value: no compiler wait on the loads below
+      float rn;
+      qf[j] = l2_normalize(__builtin_bit_cast(uint4, v), rn, sc2);
+      rows[j] = qrow[j];
+    }
+    const int wh = cwh, ww = cww;
+    if (++cww == g.nWw) {
+      cww = 0;
+      if (++cwh == g.nWh) {
+        cwh = 0;
+        ++cb;
+      }
+    }
+    if (w + 1 < w1) {
+      issue(cb, cwh, cww, sbase + (uint32_t)((cur ^ 1) * F::BUF));
+      load_q(cb, cwh, cww);
+    }
+    lds_barrier();  // k^ normalised
+
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    // S' of (chunk c, half t, tile j) with this lane's 4 keys kp .. kp + 3 (one window row);
+    // ky / kx: their window row and first column
+    auto scores = [&](auto edge_t, int c, int t, int j, const uint4& kf, int ky, int kx) {
+      constexpr bool EDGE = decltype(edge_t)::value;
+      const float* tp = mtab + (tq0 - F::DR * j + ky * K::R + kx);
       hvk_f32x4 s = hvk_mfma16(kf, qf[j], hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
-      hvk_settle(s);  // the unmasked path branches over the mask code to its readers
-      if (edge) {  // wave-uniform: last window row / column of a shifted block only
-        const bool rmis = edge_r && ((ky >= lim) != qi[j].r);
+      if (EDGE) {
+        const int qy = qy0 + (F::DQ / WIN) * j;
+        const bool rmis = edge_r && ((ky >= lim) != (qy >= lim));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool cmis = edge_c && ((kx + r >= lim) != qi[j].c);
+          const bool cmis = edge_c && ((kx + r >= lim) != (qx >= lim));
           s[r] += (rmis || cmis) ? mask2 : 0.f;
         }
       }
       if (K::N % 32 != 0 && c == K::NC - 1) {
+        const int kp = 32 * c + 16 * t + 4 * gq;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (kp + r >= K::N) s[r] = -INFINITY;
       }
       return s;
     };
+    const uint4 one_full = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+    const uint4 one_last = K::N % 32 != 0 ? ones(K::NC - 1) : one_full;
+    auto run = [&](auto edge_t) {
+      hvk_f32x4 o[QT][2], ls[QT];
 #pragma unroll
-    for (int j = 0; j < K::QB; ++j) {
-      l[j] = 0.f;
-      o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
-    }
-#pragma unroll 3
-    for (int c = 0; c < K::NC; ++c) {
-      const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
-      const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
-      const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+      for (int j = 0; j < QT; ++j) o[j][0] = o[j][1] = ls[j] = hvk_f32x4{0, 0, 0, 0};
+      // one chunk: K / V fragments read once for the QT tiles
+      auto chunk = [&](int c, const int (&ky)[2], const int (&kx)[2]) {
+        const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
+        const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
+        const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+        const uint4 one = (K::N % 32 != 0 && c == K::NC - 1) ? one_last : one_full;
 #pragma unroll
-      for (int j = 0; j < K::QB; ++j) {
-        hvk_f32x4 s0 = scores(c, 0, j, kf0), s1 = scores(c, 1, j, kf1);
-        float p[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          p[r] = __builtin_amdgcn_exp2f(s0[r]);
-          p[4 + r] = __builtin_amdgcn_exp2f(s1[r]);
-        }
-        l[j] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
-        const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
-                                    hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
-        o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
-        o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < K::QB; ++j) {
-      l[j] = hvk_group4_sum(l[j]);
-      float lshift = 0.f;  // the slow path's row max, on top of M_h
-      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l[j] >= 0x1p-100f)) != 0, 0)) {
-        // slow path (rare, wave-uniform): this tile again with the true running max
-        float m = -INFINITY;
-        l[j] = 0.f;
-        o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
-#pragma unroll 1
-        for (int c = 0; c < K::NC; ++c) {
-          const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
-          const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
-          const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
-          hvk_f32x4 s0 = scores(c, 0, j, kf0), s1 = scores(c, 1, j, kf1);
-          float mc = -INFINITY;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s0[r], s1[r]));
-          mc = hvk_group4_max(mc);
-          const float mn = fmaxf(m, mc);
-          const float alpha = __builtin_amdgcn_exp2f(m - mn);
-          m = mn;
-          float p[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            p[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
-            p[4 + r] = __builtin_amdgcn_exp2f(s1[r] - mn);
-          }
-          l[j] = l[j] * alpha + ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
-          o[j][0] *= alpha;
-          o[j][1] *= alpha;
-          const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
-                                      hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+        for (int j = 0; j < QT; ++j) {
+          const hvk_f32x4 s0 = scores(edge_t, c, 0, j, kf0, ky[0], kx[0]);
+          const hvk_f32x4 s1 = scores(edge_t, c, 1, j, kf1, ky[1], kx[1]);
+          const uint4 pf = make_uint4(
+              hvk_pack2(__builtin_amdgcn_exp2f(s0[0]), __builtin_amdgcn_exp2f(s0[1])),
+              hvk_pack2(__builtin_amdgcn_exp2f(s0[2]), __builtin_amdgcn_exp2f(s0[3])),
+              hvk_pack2(__builtin_amdgcn_exp2f(s1[0]), __builtin_amdgcn_exp2f(s1[1])),
+              hvk_pack2(__builtin_amdgcn_exp2f(s1[2]), __builtin_amdgcn_exp2f(s1[3])));
+          ls[j] = hvk_mfma16(one, pf, ls[j]);
           o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
           o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
         }
-        l[j] = hvk_group4_sum(l[j]);
-        lshift = m;
-        hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
+      };
+      if constexpr (F::PER > 0) {
+        // PER chunks span whole window rows: the lane's key rows / columns repeat with it
+#pragma unroll 1
+        for (int cg = 0; cg < K::NC / F::PER; ++cg) {
+#pragma unroll
+          for (int c2 = 0; c2 < F::PER; ++c2) {
+            int ky[2], kx[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const int kq = 32 * c2 + 16 * t + 4 * gq;  // position inside the period
+              ky[t] = (32 * F::PER / WIN) * cg + kq / WIN;
+              kx[t] = kq % WIN;
+            }
+            chunk(F::PER * cg + c2, ky, kx);
+          }
+        }
+      } else {
+#pragma unroll 1
+        for (int c = 0; c < K::NC; ++c) {
+          int ky[2], kx[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const int kp = 32 * c + 16 * t + 4 * gq;
+            ky[t] = kp / WIN;
+            kx[t] = kp - ky[t] * WIN;
+          }
+          chunk(c, ky, kx);
+        }
       }
-      // LSE: the query's log2 row constant L2 = M_h + row max + log2(row sum) for the backward
-      if (LSE && gq == 0) a.lse[(size_t)qrow[j] * g.nH + h] = Mh + lshift + __log2f(l[j]);
-      const float inv = __builtin_amdgcn_rcpf(l[j]);
-      const uint4 pk = make_uint4(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv),
-                                  hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv),
-                                  hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv),
-                                  hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv));
-      hvk_st16(a.out + (size_t)qrow[j] * C + h * 32 + 8 * gq, pk);
-    }
+#pragma unroll
+      for (int j = 0; j < QT; ++j) {
+        float l = ls[j][0];
+        float lshift = 0.f;  // the slow path's row max, on top of M_h
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
+          // slow path (rare, wave-uniform): this tile again with the true running max
+          float m = -INFINITY;
+          l = 0.f;
+          o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll 1
+          for (int c = 0; c < K::NC; ++c) {
+            const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
+            const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
+            const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+            const int kp0 = 32 * c + 4 * gq, kp1 = kp0 + 16;
+            hvk_f32x4 s0 = scores(edge_t, c, 0, j, kf0, kp0 / WIN, kp0 % WIN);
+            hvk_f32x4 s1 = scores(edge_t, c, 1, j, kf1, kp1 / WIN, kp1 % WIN);
+            hvk_settle(s0, s1);
+            float mc = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s0[r], s1[r]));
+            mc = hvk_group4_max(mc);
+            const float mn = fmaxf(m, mc);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);
+            m = mn;
+            float p[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
+              p[4 + r] = __builtin_amdgcn_exp2f(s1[r] - mn);
+            }
+            l = l * alpha + ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+            o[j][0] *= alpha;
+            o[j][1] *= alpha;
+            const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                        hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+            o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
+            o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
+          }
+          l = hvk_group4_sum(l);
+          lshift = m;
+          hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
+        }
+        // LSE: the query's log2 row constant L2 = M_h + row max + log2(row sum) for the backward
+        if (LSE && gq == 0) a.lse[(size_t)rows[j] * g.nH + h] = Mh + lshift + __log2f(l);
+        const float inv = __builtin_amdgcn_rcpf(l);
+        // accumulator rows: channels 4gq + r (o[0]) and 16 + 4gq + r (o[1]); one permlane swap
+        // per dword gives the lane 8 consecutive channels (one 16-B store)
+        const uint4 pk = hvk_pair_swap(
+            make_uint2(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv), hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv)),
+            make_uint2(hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv), hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv)));
+        hvk_st16(a.out + (size_t)rows[j] * C + h * 32 + hvk_pair_col(gq), pk);
+      }
+    };
+    if (edge_r || edge_c)
+      run(std::true_type{});
+    else
+      run(std::false_type{});
   }
 }
 
 // ----------------------------------------------------------------------------- backward
-// Normalize-backward of a head row: x^ = x * rn; dx = (dx^ - x^ (x^ . dx^)) * rn, with the
-// lane's 8 values of dx^ (times `post`) at d = 16dt + 4g + r (accumulator order).  x is
-// re-read from global (L2) in that order.  Every lane must call it (group reduction inside); `x` must point at a real row; only the
-// store (and the column-sum accumulation into acc, when non-null) is skipped when dst is null.
+// Persistent workgroups (8 waves: the 8 private CPB-gradient bin copies fit beside the images),
+// one head each over a run of windows: the head's table and bound are set up once, the bins,
+// the logit-scale and q_bias gradients accumulate over the whole run and are flushed once.
+// Per window, two phases over one LDS image pair:
+//   phase 1, query on the lane (k^ / v images, contiguous query tiles): S' and dP by MFMA,
+//     P = exp2(S' - L2) from the forward's row constant (LSE) or from a row-statistics pass,
+//     dS = P (dP - delta_O) with delta_O = dO . O, dQ = scale sum_k dS k^; with LSE the exact
+//     delta = sum P dP / sum P misses delta_O by corr = rowsum(dS) / rowsum(P), which is taken
+//     out of dQ (scale corr sum_k P k^) and handed to phase 2 with the exact delta;
+//   phase 2, key on the lane (q^ scale log2e / dO images, strided key tiles: positions
+//     kt + NT li, so a batch of bin updates never repeats a bin, tools/large_bins_check.py):
+//     the EXACT dS = P (dP - delta) gives dK, dV, the CPB-table gradient (private bins, plain
+//     LDS read-add-write) and the logit-scale gradient.
+// The next images are loaded into registers while the current phase computes (phase 1 loads
+// phase 2's q / dO rows, phase 2 the next window's k / v rows) and written to LDS between the
+// phases; every tile's own global inputs are loaded one tile ahead.  Interior windows and
+// unshifted blocks run mask-free copies of both loops.
+template <int WIN>
+struct BCfg {
+  using K = LCfg<WIN>;
+  static constexpr int WAVES = 8;
+  static constexpr int BLK = K::ROWS / 16;                    // 16-row blocks per image
+  static constexpr int PB = (BLK + WAVES - 1) / WAVES;        // blocks a wave stages per image
+  static constexpr int RRP = (K::RR + 3) / 4 * 4;             // bins per private copy
+  static constexpr int BATCH = WIN == 24 ? 8 : (WIN == 16 ? 4 : 1);  // exact read-add-write batch
+  static constexpr size_t LDS = 2 * (size_t)K::IMG + (size_t)K::TABM * 4 + (size_t)WAVES * RRP * 4 +
+                                2 * (size_t)K::ROWS * 4 + 64;
+};
 
-__device__ __forceinline__ void normalize_bwd_store(const hvk_bf16* x, float rn, const hvk_f32x4 dxh[2],
-                                                    hvk_bf16* dst, float post, int g,
-                                                    float (*acc)[4]) {
-  float xh[2][4], dot = 0.f;
+// 8 f32 of a 16x16 accumulator pair (rows 4gq + r of tile 0 = channels 4gq + r, of tile 1 =
+// channels 16 + 4gq + r) -> this lane's 8 consecutive channels from hvk_pair_col(gq)
+__device__ __forceinline__ void pair_swap_f32(const hvk_f32x4& t0, const hvk_f32x4& t1, float v[8]) {
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const uint2 v = *reinterpret_cast<const uint2*>(x + 16 * dt + 4 * g);
-    xh[dt][0] = hvk_lo(v.x) * rn; xh[dt][1] = hvk_hi(v.x) * rn;
-    xh[dt][2] = hvk_lo(v.y) * rn; xh[dt][3] = hvk_hi(v.y) * rn;
+  for (int r = 0; r < 4; r += 2) {
+    const uint4 s = hvk_pair_swap(make_uint2(__float_as_uint(t0[r]), __float_as_uint(t0[r + 1])),
+                                  make_uint2(__float_as_uint(t1[r]), __float_as_uint(t1[r + 1])));
+    // hvk_pair_swap(lo pair, hi pair) -> (lo.x', lo.y', hi.x', hi.y') in channel order 2r, 2r+1 of
+    // each half: output (a0, b0, a1, b1) = channels (r, r+1) of the first four, then of the last four
+    v[r] = __uint_as_float(s.x);
+    v[r + 1] = __uint_as_float(s.y);
+    v[4 + r] = __uint_as_float(s.z);
+    v[4 + r + 1] = __uint_as_float(s.w);
+  }
+}
+
+// Normalize-backward of one head row and a 16-B store: x^ = x rn, dx = (dx^ post - x^ (x^ . dx^
+// post)) rn over the lane's 8 channels (x: the raw row slice at hvk_pair_col(gq), dxh: the same
+// channels); the 4 lanes of the row reduce the dot product.  acc (optional): column sums.
+__device__ __forceinline__ void normalize_bwd16(const uint4& xraw, float rn, const float dxh[8], float post,
+                                                hvk_bf16* dst, float* acc) {
+  float x[8], dot = 0.f;
+  hvk_unpack8(xraw, x);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) dot += xh[dt][r] * dxh[dt][r] * post;
+  for (int e = 0; e < 8; ++e) {
+    x[e] *= rn;
+    dot = fmaf(x[e], dxh[e] * post, dot);
   }
   dot = hvk_group4_sum(dot);
   if (rn >= 1e12f) dot = 0.f;  // ||x|| <= eps: x / eps, no projection term
+  float v[8];
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    float v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = (dxh[dt][r] * post - xh[dt][r] * dot) * rn;
-    if (dst) {
-      hvk_st8(dst + 16 * dt + 4 * g, make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3])));
-      if (acc) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[dt][r] += v[r];
-      }
-    }
+  for (int e = 0; e < 8; ++e) {
+    v[e] = (dxh[e] * post - x[e] * dot) * rn;
+    if (acc) acc[e] += v[e];
   }
+  hvk_st16(dst, hvk_pack8(v));
 }
 
-template <int WIN>
-constexpr size_t bwd_large_lds() {
-  using K = LCfg<WIN>;
-  const size_t bins = HVK_LARGE_BINS ? (size_t)K::BWAVES * K::RRP : (size_t)K::RR;
-  return 2 * (size_t)K::IMG + (size_t)K::TABM * 4 + bins * 4 + 2 * (size_t)K::ROWS * 4 + 64;
-}
-
-// Logits relative to the head bound, as the forward: S' = sc2 cos + log2e bias - M_h from one
-// MFMA with the mirrored CPB table as its C operand (4 ascending floats for the lane's 4
-// consecutive keys in phase 1; 4 descending for its 4 consecutive queries in phase 2), plus
-// the -100 mask on edge windows (wave-uniform branch).  Phase 1 loop A exponentiates S'
-// directly (S' <= 0) and falls back to a running row max only for a tile whose row sum
-// underflows; the row constants kept for loop B and phase 2 are relative to M_h.
 template <int WIN, bool LSE>
-__global__ __launch_bounds__(LCfg<WIN>::BTHREADS, 1) void wmsa_bwd_large_kernel(BwdArgs a) {
+__global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kernel(BwdArgs a) {
   using K = LCfg<WIN>;
+  using F = BCfg<WIN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WmsaGeom& g = a.g;
-  int w, h;
-  hvk_decode_chunk_head(blockIdx.x, g.nH, w, h);
-  if (w >= g.n_windows) return;
+  int chunk, h;
+  if (!decode_item(g, blockIdx.x, chunk, h)) return;
+  const int w0 = (int)((long long)chunk * g.n_windows / g.n_chunks);
+  const int w1 = (int)((long long)(chunk + 1) * g.n_windows / g.n_chunks);
+  if (w0 >= w1) return;
   char* img0 = smem;
   char* img1 = smem + K::IMG;
   float* mtab = reinterpret_cast<float*>(smem + 2 * K::IMG);  // [TABM] mirrored, - M_h
-  float* dtab = mtab + K::TABM;  // [BWAVES][RRP] private bins (HVK_LARGE_BINS) or [RR] shared
-  constexpr int NBIN = HVK_LARGE_BINS ? K::BWAVES * K::RRP : K::RR;
-  float* lse_s = dtab + NBIN;    // [ROWS] row constant relative to M_h (+inf: padding rows)
-  float* dlt_s = lse_s + K::ROWS;  // [ROWS] delta = rowsum(P * dP)
-  float* red = dlt_s + K::ROWS;  // [16] max-bias partials
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+  float* bins = mtab + K::TABM;                               // [WAVES][RRP] private copies
+  float* lse_s = bins + F::WAVES * F::RRP;                    // [ROWS] row constant rel. to M_h
+  float* dlt_s = lse_s + K::ROWS;                             // [ROWS] exact delta
+  float* red = dlt_s + K::ROWS;                               // [16]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int li = lane & 15, gq = lane >> 4;
   const int C = g.C, C3 = 3 * C;
   const int per_img = g.nWh * g.nWw;
-  const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
   const float scale = a.scale[h];
   const float sc2 = scale * HVK_LOG2E;
   const float mask2 = -100.f * HVK_LOG2E;
   const int lim = WIN - g.shift;
-  const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
-  const bool edge = HVK_LARGE_PROBE == 3 ? false : (edge_r || edge_c);  // probe 3: no mask (not exact)
+  const int pcol = hvk_pair_col(gq);  // the lane's 8 output channels after the pair swap
 
   const float* bsrc = a.bias + (size_t)h * K::RR;
   float mb = -INFINITY;
-  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) mb = fmaxf(mb, bsrc[e]);
+  for (int e = threadIdx.x; e < K::RR; e += 64 * F::WAVES) mb = fmaxf(mb, bsrc[e]);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
   if (lane == 0) red[wave] = mb;
-  for (int e = threadIdx.x; e < NBIN; e += K::BTHREADS) dtab[e] = 0.f;
-  for (int e = threadIdx.x; e < K::ROWS; e += K::BTHREADS) {
-    lse_s[e] = INFINITY;
+  for (int e = threadIdx.x; e < F::WAVES * F::RRP; e += 64 * F::WAVES) bins[e] = 0.f;
+  for (int e = threadIdx.x; e < K::ROWS; e += 64 * F::WAVES) {
+    lse_s[e] = INFINITY;  // padding queries (w12): P = 0 in phase 2
     dlt_s[e] = 0.f;
   }
-  // phase-1 images: k^ and v, natural head_dim order
-  for (int t = wave; t < 2 * K::NC; t += K::BWAVES) {
-    const int pos = 16 * t + li;
-    uint4 kv = make_uint4(0, 0, 0, 0), vv = kv;
-    if (pos < K::N) {
-      const hvk_bf16* p = a.qkv + (size_t)window_token_row(g, b, wh, ww, WIN, pos) * C3 + h * 32 + 8 * gq;
-      kv = hvk_ld16(p + C);
-      vv = hvk_ld16(p + 2 * C);
+
+  // image staging through registers: a wave's blocks blk = wave + WAVES j, lane (li, gq) owns row
+  // 16 blk + li, 16-B column gq (written at fm16: conflict free); padding rows load the
+  // window's first token (finite; masked to -inf / weighted by P = 0)
+  uint4 ra[F::PB], rb[F::PB];
+  auto load_rows = [&](int b, int wh, int ww, int pa, int pbp) {  // parts (0 q, 1 k, 2 v) / dO
+#pragma unroll
+    for (int j = 0; j < F::PB; ++j) {
+      const int blk = wave + F::WAVES * j;
+      if (blk < F::BLK) {
+        int pos = 16 * blk + li;
+        if (K::ROWS != K::N) pos = pos < K::N ? pos : 0;
+        const size_t row = window_token_row(g, b, wh, ww, WIN, pos);
+        ra[j] = hvk_ld16(a.qkv + row * C3 + pa * C + h * 32 + 8 * gq);
+        rb[j] = pbp < 0 ? hvk_ld16(a.dout + row * C + h * 32 + 8 * gq)
+                        : hvk_ld16(a.qkv + row * C3 + pbp * C + h * 32 + 8 * gq);
+      }
     }
-    float rn;
-    kv = l2_normalize(kv, rn);
-    *reinterpret_cast<uint4*>(img0 + fm16(pos, gq)) = kv;
-    *reinterpret_cast<uint4*>(img1 + fm16(pos, gq)) = vv;
-  }
+  };
+  auto write_rows = [&](float post) {  // ra normalised (times post), rb raw
+#pragma unroll
+    for (int j = 0; j < F::PB; ++j) {
+      const int blk = wave + F::WAVES * j;
+      if (blk < F::BLK) {
+        float rn;
+        const int off = fm16(16 * blk + li, gq);
+        *reinterpret_cast<uint4*>(img0 + off) = l2_normalize(ra[j], rn, post);
+        *reinterpret_cast<uint4*>(img1 + off) = rb[j];
+      }
+    }
+  };
+
+  int cb = w0 / per_img, cwh = (w0 % per_img) / g.nWw, cww = w0 % g.nWw;
+  load_rows(cb, cwh, cww, 1, 2);  // k, v of the first window
   __syncthreads();
   float Mh = red[0];
 #pragma unroll
-  for (int i = 1; i < K::BWAVES; ++i) Mh = fmaxf(Mh, red[i]);
+  for (int i = 1; i < F::WAVES; ++i) Mh = fmaxf(Mh, red[i]);
   Mh = Mh * HVK_LOG2E + sc2;
-  for (int e = threadIdx.x; e < K::TABM; e += K::BTHREADS) {
+  for (int e = threadIdx.x; e < K::TABM; e += 64 * F::WAVES) {
     const int i = K::RR - 1 - e;
     mtab[e] = i >= 0 ? bsrc[i] * HVK_LOG2E - Mh : 0.f;
   }
-  __syncthreads();
+  write_rows(1.f);
+  lds_barrier();
 
-  // ---------------- phase 1: query tiles (query on the lane)
-  float dscale = 0.f;
-  float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  for (int qt = wave; qt < K::NT; qt += K::BWAVES) {
-    // query tile qt = positions qt + NT*li (N = 16 NT for w 12/16/24): the 16 queries of a tile
-    // lie >= one window row apart, so the CPB-gradient bins of one read-add-write batch are
-    // distinct across the lanes (loop B)
-    const int pos = qt + K::NT * li;
-    const int qrow = window_token_row(g, b, wh, ww, WIN, pos);
-    const hvk_bf16* qp = a.qkv + (size_t)qrow * C3 + h * 32;
-    const uint4 qraw = hvk_ld16(qp + 8 * gq);
-    const uint4 dof = hvk_ld16(a.dout + (size_t)qrow * C + h * 32 + 8 * gq);
-    float rnq;
-    const uint4 qs = l2_normalize(qraw, rnq, sc2);
-    const PosInfo<WIN> qi = query_info<WIN>(pos, lim);
-    const float* tq = mtab + (K::RR - 1 - qi.b);  // + kb(key) + r
-
-    // S' (masked; padding keys -inf) and dP - 0 of chunk c, half t; c4 = the bias C operand
-    auto tile = [&](int c, int t, hvk_f32x4& s, hvk_f32x4& d, hvk_f32x4& c4) {
-      const int kt = 2 * c + t, kp = 16 * kt + 4 * gq;
-      const int ky = kp / WIN, kx = kp - ky * WIN;
-      const float* tp = tq + ky * K::R + kx;
-      c4 = hvk_f32x4{tp[0], tp[1], tp[2], tp[3]};
-      s = hvk_mfma16(lds16(img0, fm16(16 * kt + li, gq)), qs, c4);
-      d = hvk_mfma16(lds16(img1, fm16(16 * kt + li, gq)), dof, hvk_f32x4{0, 0, 0, 0});
-      hvk_settle(s, d);  // the unmasked path branches over the mask code to their readers
-      if (edge) {  // wave-uniform; selects, not branches, per element
-        const bool rmis = edge_r && ((ky >= lim) != qi.r);
+  const uint4 one_full = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  auto ones_c = [&](int c) {  // 1.0 for the real positions of chunk c in k-slot order
+    if (K::N % 32 == 0 || c != K::NC - 1) return one_full;
+    uint32_t wv[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool cmis = edge_c && ((kx + r >= lim) != qi.c);
-          s[r] += (rmis || cmis) ? mask2 : 0.f;
-        }
+    for (int jj = 0; jj < 4; ++jj) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * jj + e;
+        const int p = 32 * c + (j < 4 ? 4 * gq + j : 16 + 4 * gq + j - 4);
+        if (p < K::N) v |= 0x3F80u << (16 * e);
       }
-      if (K::N % 32 != 0 && c == K::NC - 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (kp + r >= K::N) s[r] = -INFINITY;
-      }
-    };
-
-    // LSE: the forward's row constant and delta_O = dO . O from its output; loop B then
-    // measures how far its dS row sums miss zero and corrects delta, dQ and the logit-scale
-    // gradient exactly (the CPB gradient keeps the small remainder)
-    float lse_in = 0.f, dlt_o = 0.f;
-    if (LSE) {
-      lse_in = a.lse[(size_t)qrow * g.nH + h] - Mh;
-      float fd[8], fo[8];
-      hvk_unpack8(dof, fd);
-      hvk_unpack8(hvk_ld16(a.out + (size_t)qrow * C + h * 32 + 8 * gq), fo);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dlt_o = fmaf(fd[e], fo[e], dlt_o);
-      dlt_o = hvk_group4_sum(dlt_o);
+      wv[jj] = v;
     }
-    // loop A: row sum and delta against the head bound
-    float l = HVK_LARGE_PROBE == 6 ? 1.f : 0.f, dacc = 0.f, m = 0.f;
+    return make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  };
+  // run fn(c, ky[2], kx[2]) over the chunks, ky / kx the window row and first column of the
+  // lane's 4 positions 32c + 16t + 4gq .. +3 (periods of whole rows where the chunks allow)
+  constexpr int PER = (32 * 3) % WIN == 0 && K::NC % 3 == 0 ? 3 : (32 % WIN == 0 ? 1 : 0);
+  auto for_chunks = [&](auto&& fn) {
+    if constexpr (PER > 0) {
 #pragma unroll 1
-    for (int c = 0; c < (HVK_LARGE_PROBE == 6 || LSE ? 0 : K::NC); ++c) {
+      for (int cg = 0; cg < K::NC / PER; ++cg) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        hvk_f32x4 s, d, c4;
-        tile(c, t, s, d, c4);
+        for (int c2 = 0; c2 < PER; ++c2) {
+          int ky[2], kx[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[r]);
-          l += p;
-          dacc = fmaf(p, d[r], dacc);
+          for (int t = 0; t < 2; ++t) {
+            const int kq = 32 * c2 + 16 * t + 4 * gq;
+            ky[t] = (32 * PER / WIN) * cg + kq / WIN;
+            kx[t] = kq % WIN;
+          }
+          fn(PER * cg + c2, ky, kx);
         }
       }
-    }
-    l = hvk_group4_sum(l);
-    dacc = hvk_group4_sum(dacc);
-    if (!LSE && __builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
-      // slow path (rare, wave-uniform): row max, sum and delta with a running max
-      m = -INFINITY;
-      l = 0.f;
-      dacc = 0.f;
+    } else {
 #pragma unroll 1
       for (int c = 0; c < K::NC; ++c) {
-        hvk_f32x4 s[2], d[2], c4;
-        tile(c, 0, s[0], d[0], c4);
-        tile(c, 1, s[1], d[1], c4);
-        float mc = -INFINITY;
+        int ky[2], kx[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s[0][r], s[1][r]));
-        mc = hvk_group4_max(mc);
-        const float mn = fmaxf(m, mc);
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
-        m = mn;
-        float ps = 0.f, pd = 0.f;
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = __builtin_amdgcn_exp2f(s[t][r] - mn);
-            ps += p;
-            pd = fmaf(p, d[t][r], pd);
-          }
-        l = l * alpha + ps;
-        dacc = dacc * alpha + pd;
+        for (int t = 0; t < 2; ++t) {
+          const int kp = 32 * c + 16 * t + 4 * gq;
+          ky[t] = kp / WIN;
+          kx[t] = kp - ky[t] * WIN;
+        }
+        fn(c, ky, kx);
       }
-      l = hvk_group4_sum(l);
-      dacc = hvk_group4_sum(dacc);
     }
-    const float lse = LSE ? lse_in : m + __log2f(l);  // relative to M_h
-    const float delta = LSE ? dlt_o : dacc / l;
+  };
 
-    // loop B: dS, dQ^, bias / scale gradients
-    hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    float lk = 0.f, pp = 0.f, ps = 0.f;  // LSE: row sums of dS, P and P * sc2 cos
-#pragma unroll 1
-    for (int c = 0; c < (HVK_LARGE_PROBE == 5 ? 0 : K::NC); ++c) {
-      float ds[2][4], pl[2][4];
-      int bidx[2][4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        hvk_f32x4 s, d, c4;
-        tile(c, t, s, d, c4);
-        const int kp = 32 * c + 16 * t + 4 * gq, ky = kp / WIN, kx = kp - ky * WIN;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool kvalid = kp + r < K::N;
-          const float p = __builtin_amdgcn_exp2f(s[r] - lse);  // padding keys: exp2(-inf) = 0
-          const float dsv = p * (d[r] - delta);
-          ds[t][r] = dsv;
-          bidx[t][r] = qi.b - (ky * K::R + kx + r);
-          if (kvalid) dscale += dsv * (s[r] - c4[r]);  // sc2 * cos (the mask only where p ~ 0)
-          if (LSE) {
-            pl[t][r] = p;
-            lk += dsv;
-            pp += p;
-            if (kvalid) ps = fmaf(p, s[r] - c4[r], ps);
-          }
-        }
+  float dscale = 0.f;  // sum dS (S' - c) over the run = sc2 sum dS cos
+  float dqb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float* pb = bins + wave * F::RRP;
+
+  for (int w = w0; w < w1; ++w) {
+    const int b = cb, wh = cwh, ww = cww;
+    if (++cww == g.nWw) {
+      cww = 0;
+      if (++cwh == g.nWh) {
+        cwh = 0;
+        ++cb;
       }
-      // CPB-table gradient: this wave's own bins (plain LDS read-add-write, no float atomics).
-      // A batch of read-add-writes is exact when no two of its (lane, element) pairs share a
-      // bin: with the strided query tiles that holds for a whole 32-key chunk at w24, for each
-      // 16-key half at w16, per element at w12 (tools/large_bins_check.py); LDS operations of a
-      // wave complete in order, and the compiler fences keep hipcc from merging the reads of
-      // one batch ahead of another's writes (exact per lane, but it loses other lanes' updates)
-      if (HVK_LARGE_PROBE >= 1) {
-      } else if (HVK_LARGE_BINS) {
-        float* pb = dtab + wave * K::RRP;
-        constexpr int BATCH = WIN == 24 ? 8 : (WIN == 16 ? 4 : 1);
-#pragma unroll
-        for (int b0 = 0; b0 < 8; b0 += BATCH) {
-          float v[BATCH];
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int e = 0; e < BATCH; ++e) {
-            const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
-            const bool ok = 32 * c + 16 * t + 4 * gq + r < K::N;
-            v[e] = ok ? pb[bidx[t][r]] : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < BATCH; ++e) {
-            const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
-            const bool ok = 32 * c + 16 * t + 4 * gq + r < K::N;
-            if (ok) pb[bidx[t][r]] = v[e] + ds[t][r];
-          }
-          asm volatile("" ::: "memory");
-        }
+    }
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    const bool edge = edge_r || edge_c;
+    load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
+
+    // ---------------- phase 1: query tiles qt = wave + WAVES j (positions 16 qt + li)
+    struct QIn {
+      uint4 q, qx, dof, o;
+      float lse;
+      int row;
+    };
+    auto load_qt = [&](int qt) {
+      QIn t;
+      t.row = window_token_row(g, b, wh, ww, WIN, 16 * qt + li);
+      const hvk_bf16* qp = a.qkv + (size_t)t.row * C3 + h * 32;
+      t.q = hvk_ld16(qp + 8 * gq);
+      t.qx = hvk_ld16(qp + pcol);
+      t.dof = hvk_ld16(a.dout + (size_t)t.row * C + h * 32 + 8 * gq);
+      if (LSE) {
+        t.o = hvk_ld16(a.out + (size_t)t.row * C + h * 32 + 8 * gq);
+        t.lse = a.lse[(size_t)t.row * g.nH + h];
       } else {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (32 * c + 16 * t + 4 * gq + r < K::N)
-              atomicAdd(&dtab[bidx[t][r]], ds[t][r]);  // LDS float atomic (ds_add_f32)
+        t.o = make_uint4(0, 0, 0, 0);
+        t.lse = 0.f;
       }
-      const uint4 bf = make_uint4(hvk_pack2(scale * ds[0][0], scale * ds[0][1]),
-                                  hvk_pack2(scale * ds[0][2], scale * ds[0][3]),
-                                  hvk_pack2(scale * ds[1][0], scale * ds[1][1]),
-                                  hvk_pack2(scale * ds[1][2], scale * ds[1][3]));
-      const uint4 kf0 = tr_frag(img0, c, 0, li, gq), kf1 = tr_frag(img0, c, 1, li, gq);
-      dq[0] = hvk_mfma16(kf0, bf, dq[0]);
-      dq[1] = hvk_mfma16(kf1, bf, dq[1]);
-      if (LSE) {  // sum_k P k^ of this query tile, for the dQ correction
-        const uint4 pf = make_uint4(hvk_pack2(pl[0][0], pl[0][1]), hvk_pack2(pl[0][2], pl[0][3]),
-                                    hvk_pack2(pl[1][0], pl[1][1]), hvk_pack2(pl[1][2], pl[1][3]));
-        pk[0] = hvk_mfma16(kf0, pf, pk[0]);
-        pk[1] = hvk_mfma16(kf1, pf, pk[1]);
-      }
-    }
-    float dlt = delta;
-    if (LSE) {
-      // dS = P (dP - delta_O) misses the exact P (dP - sum P dP / sum P) by P corr per row,
-      // corr = rowsum(dS) / rowsum(P): take it out of dQ (scale corr sum_k P k^) and of the
-      // logit-scale gradient, and hand phase 2 the exact delta
-      const float corr = hvk_group4_sum(lk) / hvk_group4_sum(pp);
-      const float psq = hvk_group4_sum(ps);
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dq[dt][r] = fmaf(-scale * corr, pk[dt][r], dq[dt][r]);
-      if (gq == 0) dscale = fmaf(-corr, psq, dscale);
-      dlt = delta + corr;
-    }
-    if (gq == 0) {
-      lse_s[pos] = lse;
-      dlt_s[pos] = dlt;
-    }
-    normalize_bwd_store(qp, rnq, dq, a.dqkv + (size_t)qrow * C3 + h * 32, 1.f, gq, dqb);
-  }
-  __syncthreads();
-
-  // phase-2 images: q^ * scale * log2e (exactly the forward's operand) and dO
-  for (int t = wave; t < 2 * K::NC; t += K::BWAVES) {
-    const int pos = 16 * t + li;
-    uint4 qv = make_uint4(0, 0, 0, 0), dv = qv;
-    if (pos < K::N) {
-      const int row = window_token_row(g, b, wh, ww, WIN, pos);
-      qv = hvk_ld16(a.qkv + (size_t)row * C3 + h * 32 + 8 * gq);
-      dv = hvk_ld16(a.dout + (size_t)row * C + h * 32 + 8 * gq);
-    }
-    float rn;
-    qv = l2_normalize(qv, rn, sc2);
-    *reinterpret_cast<uint4*>(img0 + fm16(pos, gq)) = qv;
-    *reinterpret_cast<uint4*>(img1 + fm16(pos, gq)) = dv;
-  }
-  __syncthreads();
-
-  // ---------------- phase 2: key tiles (key on the lane)
-  for (int kt = wave; kt < (HVK_LARGE_PROBE == 4 ? 0 : K::NT); kt += K::BWAVES) {
-    const int pos = 16 * kt + li;
-    const int krow = window_token_row(g, b, wh, ww, WIN, pos);
-    const hvk_bf16* kp = a.qkv + (size_t)krow * C3 + h * 32 + C;
-    const uint4 kraw = hvk_ld16(kp + 8 * gq);
-    const uint4 vf = hvk_ld16(kp + C + 8 * gq);
-    float rnk;
-    const uint4 kh = l2_normalize(kraw, rnk);
-    const PosInfo<WIN> ki = key_info<WIN>(pos, lim);
-    const float* tk = mtab + (K::RR - 1 + ki.b);  // - qb(query)
-    hvk_f32x4 dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll 1
-    for (int c = 0; c < K::NC; ++c) {
-      float p[2][4], ds[2][4];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int qt = 2 * c + t, q0 = 16 * qt + 4 * gq;  // this lane's queries q0 .. q0 + 3
-        if (K::NT % 2 == 1 && qt >= K::NT) {  // w12's padding half chunk: no queries
-#pragma unroll
-          for (int r = 0; r < 4; ++r) p[t][r] = ds[t][r] = 0.f;
-          continue;
-        }
-        const int qy = q0 / WIN, qx = q0 - qy * WIN;
-        const float* tp = tk - ((qy + WIN - 1) * K::R + qx + WIN - 1);  // entries tp[-r]
-        hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(16 * qt + li, gq)), kh,
-                                 hvk_f32x4{tp[0], tp[-1], tp[-2], tp[-3]});
-        const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(16 * qt + li, gq)), vf, hvk_f32x4{0, 0, 0, 0});
-        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
-        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);
-        const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
-        hvk_settle(s);
-        if (edge) {  // wave-uniform; selects, not branches, per element
-          const bool rmis = edge_r && (ki.r != (qy >= lim));
+      return t;
+    };
+    QIn cur = load_qt(wave);
+    for (int qt = wave; qt < K::NT; qt += F::WAVES) {
+      QIn nxt = cur;
+      if (qt + F::WAVES < K::NT) nxt = load_qt(qt + F::WAVES);
+      const int pos = 16 * qt + li;
+      const int qy = pos / WIN, qxp = pos - qy * WIN;
+      const int tq = K::RR - 1 - ((qy + WIN - 1) * K::R + qxp + WIN - 1);
+      float rnq;
+      const uint4 qs = l2_normalize(cur.q, rnq, sc2);
+      float rowc, delta;  // row constant (rel. to M_h) and delta for dS
+      // S' (masked) and dP of (chunk c, half t)
+      auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        const float* tp = mtab + (tq + ky * K::R + kx);
+        s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), qs, hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
+        d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), cur.dof, hvk_f32x4{0, 0, 0, 0});
+        if (EDGE) {
+          const bool rmis = edge_r && ((ky >= lim) != (qy >= lim));
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const bool cmis = edge_c && (ki.c != (qx + r >= lim));
+            const bool cmis = edge_c && ((kx + r >= lim) != (qxp >= lim));
             s[r] += (rmis || cmis) ? mask2 : 0.f;
           }
         }
+        if (K::N % 32 != 0 && c == K::NC - 1) {
+          const int kp = 32 * c + 16 * t + 4 * gq;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          p[t][r] = __builtin_amdgcn_exp2f(s[r] - lr[r]);  // padding query: lse = +inf -> 0
-          ds[t][r] = p[t][r] * (d[r] - dr[r]);
+          for (int r = 0; r < 4; ++r)
+            if (kp + r >= K::N) s[r] = -INFINITY;
         }
-      }
-      const uint4 pf = make_uint4(hvk_pack2(p[0][0], p[0][1]), hvk_pack2(p[0][2], p[0][3]),
-                                  hvk_pack2(p[1][0], p[1][1]), hvk_pack2(p[1][2], p[1][3]));
-      const uint4 dsf = make_uint4(hvk_pack2(ds[0][0], ds[0][1]), hvk_pack2(ds[0][2], ds[0][3]),
-                                   hvk_pack2(ds[1][0], ds[1][1]), hvk_pack2(ds[1][2], ds[1][3]));
+      };
+      if (LSE) {
+        rowc = cur.lse - Mh;
+        float fd[8], fo[8], dl = 0.f;
+        hvk_unpack8(cur.dof, fd);
+        hvk_unpack8(cur.o, fo);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        dv[dt] = hvk_mfma16(tr_frag(img1, c, dt, li, gq), pf, dv[dt]);
-        dk[dt] = hvk_mfma16(tr_frag(img0, c, dt, li, gq), dsf, dk[dt]);
+        for (int e = 0; e < 8; ++e) dl = fmaf(fd[e], fo[e], dl);
+        delta = hvk_group4_sum(dl);
+      } else {
+        // row statistics against the head bound (a running max only where the sum underflows)
+        float l = 0.f, dacc = 0.f;
+        auto statsA = [&](auto edge_t) {
+          for_chunks([&](int c, const int (&ky)[2], const int (&kx)[2]) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              hvk_f32x4 s, d;
+              tile(edge_t, c, t, ky[t], kx[t], s, d);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[r]);
+                l += p;
+                dacc = fmaf(p, d[r], dacc);
+              }
+            }
+          });
+        };
+        if (edge) statsA(std::true_type{}); else statsA(std::false_type{});
+        l = hvk_group4_sum(l);
+        dacc = hvk_group4_sum(dacc);
+        float m = 0.f;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
+          m = -INFINITY;
+          l = 0.f;
+          dacc = 0.f;
+#pragma unroll 1
+          for (int c = 0; c < K::NC; ++c) {
+            hvk_f32x4 s[2], d[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const int kp = 32 * c + 16 * t + 4 * gq;
+              if (edge) tile(std::true_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t]);
+              else tile(std::false_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t]);
+            }
+            hvk_settle(s[0], s[1], d[0], d[1]);
+            float mc = -INFINITY;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s[0][r], s[1][r]));
+            mc = hvk_group4_max(mc);
+            const float mn = fmaxf(m, mc);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);
+            m = mn;
+            float ps = 0.f, pd = 0.f;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[t][r] - mn);
+                ps += p;
+                pd = fmaf(p, d[t][r], pd);
+              }
+            l = l * alpha + ps;
+            dacc = dacc * alpha + pd;
+          }
+          l = hvk_group4_sum(l);
+          dacc = hvk_group4_sum(dacc);
+        }
+        rowc = m + __log2f(l);
+        delta = dacc / l;
       }
+      // loop B: dS, sum_k dS k^ (and with LSE sum_k P k^, sum_k P, sum_k dS)
+      hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+      hvk_f32x4 pp = {0, 0, 0, 0};
+      float lk = 0.f;
+      auto loopB = [&](auto edge_t) {
+        for_chunks([&](int c, const int (&ky)[2], const int (&kx)[2]) {
+          float p[8], ds[8];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            hvk_f32x4 s, d;
+            tile(edge_t, c, t, ky[t], kx[t], s, d);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p[4 * t + r] = __builtin_amdgcn_exp2f(s[r] - rowc);  // padding keys: 0
+              ds[4 * t + r] = p[4 * t + r] * (d[r] - delta);
+              if (LSE) lk += ds[4 * t + r];
+            }
+          }
+          const uint4 dsf = make_uint4(hvk_pack2(ds[0], ds[1]), hvk_pack2(ds[2], ds[3]),
+                                       hvk_pack2(ds[4], ds[5]), hvk_pack2(ds[6], ds[7]));
+          const uint4 kf0 = tr_frag(img0, c, 0, li, gq), kf1 = tr_frag(img0, c, 1, li, gq);
+          dq[0] = hvk_mfma16(kf0, dsf, dq[0]);
+          dq[1] = hvk_mfma16(kf1, dsf, dq[1]);
+          if (LSE) {
+            const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                        hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+            pk[0] = hvk_mfma16(kf0, pf, pk[0]);
+            pk[1] = hvk_mfma16(kf1, pf, pk[1]);
+            pp = hvk_mfma16(ones_c(c), pf, pp);
+          }
+        });
+      };
+      if (edge) loopB(std::true_type{}); else loopB(std::false_type{});
+      float dlt = delta, corr = 0.f;
+      if (LSE) {
+        corr = hvk_group4_sum(lk) / pp[0];
+        dlt = delta + corr;
+      }
+      if (gq == 0) {
+        lse_s[pos] = rowc;
+        dlt_s[pos] = dlt;
+      }
+      // dq^ = scale (sum_k dS k^ - corr sum_k P k^) in this lane's 8 output channels
+      hvk_f32x4 e0, e1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        e0[r] = scale * fmaf(-corr, pk[0][r], dq[0][r]);
+        e1[r] = scale * fmaf(-corr, pk[1][r], dq[1][r]);
+      }
+      float dxh[8];
+      pair_swap_f32(e0, e1, dxh);
+      normalize_bwd16(cur.qx, rnq, dxh, 1.f, a.dqkv + (size_t)cur.row * C3 + h * 32 + pcol, dqb);
+      cur = nxt;
     }
-    // dk^ = sum_q scale dS q^ = sum_q dS (q^ scale log2e) / log2e
-    hvk_bf16* dst = a.dqkv + (size_t)krow * C3 + h * 32;
-    normalize_bwd_store(kp, rnk, dk, dst + C, 1.f / HVK_LOG2E, gq, nullptr);
+    lds_barrier();             // phase-1 reads done; row constants published
+    write_rows(sc2);           // q^ scale log2e (exactly the forward's operand), dO
+    if (w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
+    lds_barrier();
+
+    // ---------------- phase 2: key tiles kt = wave + WAVES j (positions kt + NT li)
+    struct KIn {
+      uint4 k, kx, v;
+      int row;
+    };
+    auto load_kt = [&](int kt) {
+      KIn t;
+      t.row = window_token_row(g, b, wh, ww, WIN, kt + K::NT * li);
+      const hvk_bf16* kp = a.qkv + (size_t)t.row * C3 + C + h * 32;
+      t.k = hvk_ld16(kp + 8 * gq);
+      t.kx = hvk_ld16(kp + pcol);
+      t.v = hvk_ld16(kp + C + 8 * gq);
+      return t;
+    };
+    KIn kc = load_kt(wave);
+    for (int kt = wave; kt < K::NT; kt += F::WAVES) {
+      KIn kn = kc;
+      if (kt + F::WAVES < K::NT) kn = load_kt(kt + F::WAVES);
+      const int pos = kt + K::NT * li;
+      const int ky = pos / WIN, kxp = pos - ky * WIN;
+      const int tk = K::RR - 1 + ky * K::R + kxp;  // mirrored entry of query bq: tk - bq
+      const int bk = ky * K::R + kxp;
+      float rnk;
+      const uint4 kh = l2_normalize(kc.k, rnk);
+      hvk_f32x4 dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+      auto loop2 = [&](auto edge_t) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        for_chunks([&](int c, const int (&qyy)[2], const int (&qxx)[2]) {
+          float p[8], ds[8];
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-      hvk_st8(dst + 2 * C + 16 * dt + 4 * gq,
-              make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3])));
+          for (int t = 0; t < 2; ++t) {
+            const int q0 = 32 * c + 16 * t + 4 * gq;  // this lane's queries q0 .. q0 + 3
+            const int bq = (qyy[t] + WIN - 1) * K::R + qxx[t] + WIN - 1;
+            const float* tp = mtab + (tk - bq);  // entries tp[-r]
+            const hvk_f32x4 c4 = {tp[0], tp[-1], tp[-2], tp[-3]};
+            hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), kh, c4);
+            const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), kc.v, hvk_f32x4{0, 0, 0, 0});
+            const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
+            const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);
+            const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+            if (EDGE) {
+              const bool rmis = edge_r && ((ky >= lim) != (qyy[t] >= lim));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const bool cmis = edge_c && ((kxp >= lim) != (qxx[t] + r >= lim));
+                s[r] += (rmis || cmis) ? mask2 : 0.f;
+              }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float pr = __builtin_amdgcn_exp2f(s[r] - lr[r]);  // padding query: lse +inf
+              const float dsr = pr * (d[r] - dr[r]);
+              p[4 * t + r] = pr;
+              ds[4 * t + r] = dsr;
+              dscale = fmaf(dsr, s[r] - c4[r], dscale);
+            }
+          }
+          // CPB-table gradient: this wave's own bins, batches of BATCH elements that never share a
+          // bin across the lanes (strided key tiles); the compiler fences keep one batch's reads
+          // behind the previous batch's writes
+#pragma unroll
+          for (int b0 = 0; b0 < 8; b0 += F::BATCH) {
+            float v[F::BATCH];
+            int bi[F::BATCH];
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int e = 0; e < F::BATCH; ++e) {
+              const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
+              const int bq = (qyy[t] + WIN - 1) * K::R + qxx[t] + r + WIN - 1;
+              bi[e] = bq - bk;
+              const bool ok = K::N % 32 == 0 || 32 * c + 16 * t + 4 * gq + r < K::N;
+              v[e] = ok ? pb[bi[e]] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < F::BATCH; ++e) {
+              const int t = (b0 + e) >> 2, r = (b0 + e) & 3;
+              const bool ok = K::N % 32 == 0 || 32 * c + 16 * t + 4 * gq + r < K::N;
+              if (ok) pb[bi[e]] = v[e] + ds[b0 + e];
+            }
+            asm volatile("" ::: "memory");
+          }
+          const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                      hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+          const uint4 dsf = make_uint4(hvk_pack2(ds[0], ds[1]), hvk_pack2(ds[2], ds[3]),
+                                       hvk_pack2(ds[4], ds[5]), hvk_pack2(ds[6], ds[7]));
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            dv[dt] = hvk_mfma16(tr_frag(img1, c, dt, li, gq), pf, dv[dt]);
+            dk[dt] = hvk_mfma16(tr_frag(img0, c, dt, li, gq), dsf, dk[dt]);
+          }
+        });
+      };
+      if (edge) loop2(std::true_type{}); else loop2(std::false_type{});
+      // dk^ = sum_q scale dS q^ = sum_q dS (q^ scale log2e) / log2e
+      hvk_bf16* dst = a.dqkv + (size_t)kc.row * C3 + h * 32;
+      float dxh[8];
+      pair_swap_f32(dk[0], dk[1], dxh);
+      normalize_bwd16(kc.kx, rnk, dxh, 1.f / HVK_LOG2E, dst + C + pcol, nullptr);
+      const uint4 vk = hvk_pair_swap(make_uint2(hvk_pack2(dv[0][0], dv[0][1]), hvk_pack2(dv[0][2], dv[0][3])),
+                                     make_uint2(hvk_pack2(dv[1][0], dv[1][1]), hvk_pack2(dv[1][2], dv[1][3])));
+      hvk_st16(dst + 2 * C + pcol, vk);
+      kc = kn;
+    }
+    lds_barrier();  // phase-2 reads done
+    if (w + 1 < w1) {
+      write_rows(1.f);  // the next window's k^, v
+      lds_barrier();
+    }
   }
-  __syncthreads();
 
   float* gbias = a.dbias_acc + (size_t)h * K::RR;
-  for (int e = threadIdx.x; e < K::RR; e += K::BTHREADS) {
+  for (int e = threadIdx.x; e < K::RR; e += 64 * F::WAVES) {
     float v = 0.f;
 #pragma unroll
-    for (int c = 0; c < (HVK_LARGE_BINS ? K::BWAVES : 1); ++c) v += dtab[c * K::RRP + e];
+    for (int c = 0; c < F::WAVES; ++c) v += bins[c * F::RRP + e];
     atomicAdd(gbias + e, v);
   }
   dscale = hvk_wave_sum(dscale);
   if (lane == 0) atomicAdd(a.dscale_acc + h, dscale / sc2);
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = hvk_row16_sum(dqb[dt][r]);
-      if (li == 0) atomicAdd(a.dqb_acc + h * 32 + 16 * dt + 4 * gq + r, v);
-    }
+  for (int e = 0; e < 8; ++e) {
+    const float v = hvk_row16_sum(dqb[e]);
+    if (li == 0) atomicAdd(a.dqb_acc + h * 32 + pcol + e, v);
+  }
 }
 
 // copy the bins out, write dscale / dq_bias, leave the workspace zero
@@ -697,18 +922,19 @@ __global__ __launch_bounds__(256) void wmsa_finalize_large_kernel(BwdArgs a, flo
 }
 
 template <int WIN, bool LSE>
-int launch_fwd_large_(const FwdArgs& a, hipStream_t st) {
-  using K = LCfg<WIN>;
-  const size_t lds = 2 * (size_t)K::IMG + ((size_t)K::TABM + K::WAVES) * 4;
+int launch_fwd_large_(FwdArgs a, hipStream_t st) {
+  using F = FCfg<WIN>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_large_kernel<WIN, LSE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)F::LDS);
     attr = true;
   }
-  const int padded = (a.g.n_windows + 7) / 8 * 8;
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_large_kernel<WIN, LSE>), dim3(padded * a.g.nH),
-                   dim3(K::THREADS), lds, st, a);
+  // persistent: OCC resident workgroups per CU, n_chunks (multiple of 8) x heads of them
+  int rc = make_geom(a.g.B, a.g.H, a.g.W, a.g.C, a.g.nH, WIN, a.g.shift, 256 * F::OCC, a.g);
+  if (rc) return rc;
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_large_kernel<WIN, LSE>), dim3(a.g.n_chunks * a.g.nH),
+                   dim3(64 * F::WAVES), F::LDS, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd_large");
   return HVK_OK;
 }
@@ -718,18 +944,19 @@ int launch_fwd_large(const FwdArgs& a, hipStream_t st) {
 }
 
 template <int WIN, bool LSE>
-int launch_bwd_large_(const BwdArgs& a, hipStream_t st) {
-  using K = LCfg<WIN>;
-  const size_t lds = bwd_large_lds<WIN>();
+int launch_bwd_large_(BwdArgs a, hipStream_t st) {
+  using F = BCfg<WIN>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_large_kernel<WIN, LSE>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)F::LDS);
     attr = true;
   }
-  const int padded = (a.g.n_windows + 7) / 8 * 8;
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_large_kernel<WIN, LSE>), dim3(padded * a.g.nH),
-                   dim3(K::BTHREADS), lds, st, a);
+  // persistent: one resident workgroup per CU, n_chunks (multiple of 8) x heads of them
+  int rc = make_geom(a.g.B, a.g.H, a.g.W, a.g.C, a.g.nH, WIN, a.g.shift, 256, a.g);
+  if (rc) return rc;
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_large_kernel<WIN, LSE>), dim3(a.g.n_chunks * a.g.nH),
+                   dim3(64 * F::WAVES), F::LDS, st, a);
   return HVK_OK;
 }
 

@@ -55,10 +55,6 @@ struct RingCfg {
   static_assert(NT <= 4, "window larger than 8 needs the large-window kernels");
 };
 
-// LDS byte address of a pointer into dynamic shared memory
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
 // LDS reads issued from inline asm: the compiler's waitcnt pass does not see them, so it
 // cannot add the conservative vmcnt(0) it inserts before LDS reads while an LDS-DMA may be
 // pending (that would also wait for this workgroup's outstanding output stores).  The caller

@@ -1,7 +1,7 @@
 """Generate the golden fixtures under tests/golden/ by importing the REFERENCE
 (/root/reference, read-only) in the build container.
 
-Run:  python tests/golden/make_golden.py [--only index,modules,models,taxonomy,losses,swinb,prod]
+Run:  python tests/golden/make_golden.py [--only index,modules,models,taxonomy,losses,swinb,prod,steps]
       (needs /root/reference; CPU only)
 
 The reference's third-party imports that are absent offline are replaced by
@@ -110,6 +110,8 @@ def main():
         swinb_and_prod(ref, init_params_from_rng, "swinb")
     if "prod" in only:
         swinb_and_prod(ref, init_params_from_rng, "prod")
+    if "steps" in only:
+        train_steps(ref, ref_h, init_params_from_rng)
     if "index" not in only:
         return main_rest(ref, ref_h, only)
     # ---------------------------------------------------------------- indices
@@ -162,6 +164,7 @@ def main_rest(ref, ref_h, only):
         return p
 
     def run(m, prefix, x, seed, mask=None):
+        m.zero_grad(set_to_none=True)  # wattn_* run the same module twice
         x = x.clone().requires_grad_(True)
         y = m(x) if mask is None else m(x, mask=mask)
         g = torch.from_numpy(np.random.default_rng(seed + 1).standard_normal(
@@ -170,10 +173,10 @@ def main_rest(ref, ref_h, only):
         mods[prefix + "x"] = x.detach().numpy()
         mods[prefix + "y"] = y.detach().numpy()
         mods[prefix + "gy"] = g.numpy()
-        mods[prefix + "gx"] = x.grad.numpy()
+        mods[prefix + "gx"] = x.grad.numpy().copy()
         for k, v in m.named_parameters():
             if v.grad is not None:
-                mods[prefix + "grad." + k] = v.grad.numpy()
+                mods[prefix + "grad." + k] = v.grad.numpy().copy()  # the module may run again
 
     rng = np.random.default_rng(1234)
     # WindowAttention with a shift mask: dim 64, 2 heads (head_dim 32), w 7, res 14
@@ -410,6 +413,69 @@ def swinb_and_prod(ref, init_params_from_rng, which):
         out[f"{name}.n_state_keys"] = np.array(len(net.state_dict()))
         out[f"{name}.macs"] = np.array(net.flops(), np.float64)
     np.savez_compressed(os.path.join(HERE, "swinb_golden.npz"), **out)
+
+
+STEPS = {
+    # whole training steps (loss + every parameter gradient) of BASELINE configs[2..4]:
+    # (model cfg, batch, loss); drop_path 0 (the shim's DropPath is the identity)
+    "t_hxe": (dict(img_size=224, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24],
+                   window_size=7, num_classes=10000, drop_path_rate=0.0), 2, "hxe"),
+    "b224_mt": (SWINB["b224_mt"], 1, "multitask"),
+    "b384_hxe": (SWINB["b384_w24"], 1, "hxe"),
+}
+STEP_SAMPLES = 512
+MT_COEFFS = [8, 5.65, 4, 2.82, 2, 1.41, 1]  # configs/pretrain/r50_multitask_base.yaml:3
+
+
+def train_steps(ref, ref_h, init_params_from_rng):
+    """step_golden.npz: per config, the reference network's loss and parameter gradients for one
+    step, in f32 and under CPU bf16 autocast (the reference's own bf16 error: the tests bound
+    the HIP path by max(base, 1.5 x that error) per tensor).  Multitask: the reference's
+    MultitaskCrossEntropy (hierarchy.py:65-94).  HXE: not implemented by the reference
+    (hierarchy.py:183-185), so the loss on the reference's logits is the oracle's HXE
+    (hierarchy_ref.hxe_loss_torch, pinned by closed-form tests) -- the network half is the
+    reference's.  Gradients are stored sampled (STEP_SAMPLES entries, tests/golden_util.py);
+    the bf16 error is measured on the full tensors and stored as one number per tensor."""
+    sys.path.insert(0, REPO)
+    from oracle import hierarchy_ref
+    from hvamd.hierarchy import Taxonomy
+    tax = Taxonomy.synthetic()
+    lam = hierarchy_ref.hxe_level_weights("exponential", 0.1)
+    out = {}
+    for name, (cfg, B, loss_kind) in STEPS.items():
+        net = ref.SwinTransformerV2(**cfg).train()
+        shapes = {k: v.shape for k, v in net.state_dict().items()
+                  if k.endswith(("weight", "bias", "logit_scale")) and "relative" not in k}
+        missing, unexpected = net.load_state_dict(init_params_from_rng(shapes, 7), strict=False)
+        assert not unexpected, unexpected
+        x = torch.from_numpy(seeded(42, (B, 3, cfg["img_size"], cfg["img_size"])))
+        leaves = np.random.default_rng(43).integers(0, tax.num_leaves, B)
+        paths = tax.leaf_paths[leaves]
+        out[f"{name}.leaves"] = leaves
+
+        def loss_of(z):
+            if loss_kind == "hxe":
+                return hierarchy_ref.hxe_loss_torch(z.float(), paths, tax.perm, tax.node_start,
+                                                    tax.node_end, tax.tier_base, lam)
+            return ref_h.MultitaskCrossEntropy(coeffs=MT_COEFFS)([t.float() for t in z],
+                                                                 torch.from_numpy(paths))
+        grads = {}
+        for prec in ("f32", "bf16"):
+            net.zero_grad()
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=prec == "bf16"):
+                z = net(x)
+            loss = loss_of(z)
+            loss.backward()
+            out[f"{name}.loss_{prec}"] = np.array(float(loss))
+            grads[prec] = {k: v.grad.detach().float().clone() for k, v in net.named_parameters()
+                           if v.grad is not None}
+            print(name, prec, float(loss), flush=True)
+        for k, g32 in grads["f32"].items():
+            g16 = grads["bf16"][k]
+            out[f"{name}.g.{k}"] = sampled(f"{name}.g.{k}", g32.numpy(), STEP_SAMPLES)
+            out[f"{name}.e16.{k}"] = np.array(float((g16 - g32).norm() / g32.norm().clamp_min(1e-30)))
+        del net, grads
+    np.savez_compressed(os.path.join(HERE, "step_golden.npz"), **out)
 
 
 class _FakeDir(str):

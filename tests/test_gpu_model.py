@@ -71,6 +71,9 @@ def test_window_attention_reference_api(golden, which, seed):
     y, x = _run(wa, which, g, mask=mask)
     assert rel(y.detach().float().cpu(), g[which + "y"]) < 1e-2
     assert rel(x.grad.float().cpu(), g[which + "gx"]) < 2e-2
+    for k, p in wa.named_parameters():  # q_bias / v_bias routed through the kernel and proj
+        r = rel(p.grad.float().cpu(), g[which + "grad." + k])
+        assert r < (5e-2 if "logit_scale" in k or "cpb_mlp" in k else 2e-2), (k, r)
 
 
 def test_patch_merging_vs_reference(golden):
