@@ -22,6 +22,11 @@
 // bank-conflict free (checked with the LDS bank model of MI355X_MICROARCH.md).
 #include "wmsa_common.h"
 
+// forward row sums: 1 = a ones-vector MFMA over the bf16 P, 0 = f32 adds of P (fewer registers)
+#ifndef HVK_FWD_ROWSUM_MFMA
+#define HVK_FWD_ROWSUM_MFMA 1
+#endif
+
 namespace hvk_wmsa {
 namespace {
 
@@ -49,6 +54,50 @@ __device__ __forceinline__ uint4 tr_frag(const char* img, int c, int dt, int li,
   const uint2 lo = hvk_tr_read(reinterpret_cast<const hvk_bf16*>(img + fm8(rr, c8)));
   const uint2 hi = hvk_tr_read(reinterpret_cast<const hvk_bf16*>(img + fm8(rr + 16, c8)));
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
+}
+
+// LDS access through explicit 32-bit LDS addresses (address-space-3 pointers), so a few base
+// registers laundered per loop iteration plus compile-time offsets address every fragment
+typedef __attribute__((address_space(3))) const char lds_cchar;
+__device__ __forceinline__ lds_cchar* lds_ptr(uint32_t a) { return (lds_cchar*)(size_t)a; }
+__device__ __forceinline__ uint4 lds_ld16(uint32_t a) {
+  return __builtin_bit_cast(uint4, *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x4*>(lds_ptr(a)));
+}
+__device__ __forceinline__ hvk_f32x4 lds_ld4f(uint32_t a) {  // 4 consecutive floats (2 x ds_read2_b32)
+  const __attribute__((address_space(3))) float* f = reinterpret_cast<const __attribute__((address_space(3))) float*>(lds_ptr(a));
+  return hvk_f32x4{f[0], f[1], f[2], f[3]};
+}
+__device__ __forceinline__ uint2 lds_tr8(uint32_t a) {
+  hvk_i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) hvk_i16x4*)(lds_ptr(a)));
+  return __builtin_bit_cast(uint2, r);
+}
+__device__ __forceinline__ uint32_t launder(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// The -100 mask of a shifted block's edge window (swinv2.py:357-388, 249-254) on the 4 scores of
+// a lane: its fixed token (band bits `band`: bit 0 = last row band, bit 1 = last column band,
+// each kept only where the window is on that edge: erow / ecol) against 4 consecutive tokens
+// of one window row (row y, columns x .. x+3).  Region bits are integer arithmetic, not lane
+// masks (those pinned SGPR pairs and spilled); UNI: 4 | lim, so the 4 tokens share a region.
+template <bool UNI>
+__device__ __forceinline__ void edge_mask(hvk_f32x4& s, int y, int x, int band, int erow, int ecol, int lim,
+                                          float mask2) {
+  const int br = (int)((unsigned)(lim - 1 - y) >> 31) & erow;
+  if (UNI) {
+    const int bc = ((int)((unsigned)(lim - 1 - x) >> 31) & ecol) << 1;
+    const float m = (br | bc) != band ? mask2 : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[r] += m;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int bc = ((int)((unsigned)(lim - 1 - x - r) >> 31) & ecol) << 1;
+      s[r] += (br | bc) != band ? mask2 : 0.f;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------ forward
@@ -89,8 +138,12 @@ struct FCfg {
 // in front of LDS reads while one of its own LDS-DMAs is pending.  The kernel waits for it with
 // an explicit s_waitcnt before the barrier that publishes the buffer.
 __device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t m0) {
+  // the base and m0 are wave-uniform: make them scalar for the "s" operands
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-               :: "s"(m0), "v"(voff), "s"(base) : "memory");
+               :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
 }
 // barrier without the vmcnt(0) a __syncthreads() fence adds (the next window's DMA and
 // query loads stay in flight); LDS writes before it are waited for
@@ -148,13 +201,12 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
   // this wave's query tiles: positions 16 (wave + WAVES j) + li (bias index step DR per tile)
   const int qp0 = 16 * wave + li, qy0 = qp0 / WIN, qx = qp0 % WIN;
   const int tq0 = K::RR - 1 - ((qy0 + WIN - 1) * K::R + qx + WIN - 1);  // mirrored entry base
-  int qrow[QT];
   uint4 qn[QT];  // raw q of the next window (in flight under this window's math)
   auto load_q = [&](int b, int wh, int ww) {
 #pragma unroll
     for (int j = 0; j < QT; ++j) {
-      qrow[j] = window_token_row(g, b, wh, ww, WIN, qp0 + F::DQ * j);
-      qn[j] = hvk_ld16(a.qkv + (size_t)qrow[j] * (3 * C) + h * 32 + 8 * gq);
+      const int row = window_token_row(g, b, wh, ww, WIN, qp0 + F::DQ * j);
+      qn[j] = hvk_ld16(a.qkv + (size_t)row * (3 * C) + h * 32 + 8 * gq);
     }
   };
 
@@ -214,16 +266,14 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
     }
     // this window's queries (normalised, times scale log2e): the loads are complete
     uint4 qf[QT];
-    int rows[QT];
 #pragma unroll
     for (int j = 0; j < QT; ++j) {
       hvk_u32x4 v = __builtin_bit_cast(hvk_u32x4, qn[j]);
       asm volatile("" : "+v"(v));  // a fresh value: no compiler wait on the loads below
       float rn;
       qf[j] = l2_normalize(__builtin_bit_cast(uint4, v), rn, sc2);
-      rows[j] = qrow[j];
     }
-    const int wh = cwh, ww = cww;
+    const int b = cb, wh = cwh, ww = cww;
     if (++cww == g.nWw) {
       cww = 0;
       if (++cwh == g.nWh) {
@@ -240,18 +290,17 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
     const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
     // S' of (chunk c, half t, tile j) with this lane's 4 keys kp .. kp + 3 (one window row);
     // ky / kx: their window row and first column
+    const int erow = edge_r ? 1 : 0, ecol = edge_c ? 1 : 0;
+    // edge_t: 0 interior / unshifted, 1 edge window with 4 | lim, 2 edge window otherwise
     auto scores = [&](auto edge_t, int c, int t, int j, const uint4& kf, int ky, int kx) {
-      constexpr bool EDGE = decltype(edge_t)::value;
+      constexpr int EDGE = decltype(edge_t)::value;
       const float* tp = mtab + (tq0 - F::DR * j + ky * K::R + kx);
       hvk_f32x4 s = hvk_mfma16(kf, qf[j], hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
       if (EDGE) {
         const int qy = qy0 + (F::DQ / WIN) * j;
-        const bool rmis = edge_r && ((ky >= lim) != (qy >= lim));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool cmis = edge_c && ((kx + r >= lim) != (qx >= lim));
-          s[r] += (rmis || cmis) ? mask2 : 0.f;
-        }
+        const int band = ((int)((unsigned)(lim - 1 - qy) >> 31) & erow) |
+                         (((int)((unsigned)(lim - 1 - qx) >> 31) & ecol) << 1);
+        edge_mask<EDGE == 1>(s, ky, kx, band, erow, ecol, lim, mask2);
       }
       if (K::N % 32 != 0 && c == K::NC - 1) {
         const int kp = 32 * c + 16 * t + 4 * gq;
@@ -263,117 +312,179 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
     };
     const uint4 one_full = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
     const uint4 one_last = K::N % 32 != 0 ? ones(K::NC - 1) : one_full;
+    hvk_f32x4 o[QT][2], ls[QT];
+    // lane-constant LDS byte addresses of this window's fragments (chunk c at + 2048 c):
+    // k^ rows 32c + 16t + li, 16-B column gq (fm16: 2048 c + 1024 t + kl); V^T (tr_frag) rows
+    // 32c + 4gq + li/4 (+16), 8-B column li%4 (+4 dt) (2048 c + 1024 h + 512 dt + vl)
+    const uint32_t kl = lds_addr(kimg) + (uint32_t)fm16(li, gq);
+    const uint32_t vl = lds_addr(vimg) + (uint32_t)fm8(4 * gq + (li >> 2), li & 3);
+    const uint32_t tl = lds_addr(mtab) + 4u * (uint32_t)tq0;  // + 4 (bk(key) - DR j)
     auto run = [&](auto edge_t) {
-      hvk_f32x4 o[QT][2], ls[QT];
+      constexpr int EDGE = decltype(edge_t)::value;
 #pragma unroll
       for (int j = 0; j < QT; ++j) o[j][0] = o[j][1] = ls[j] = hvk_f32x4{0, 0, 0, 0};
-      // one chunk: K / V fragments read once for the QT tiles
-      auto chunk = [&](int c, const int (&ky)[2], const int (&kx)[2]) {
-        const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
-        const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
-        const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+      // one chunk: K / V fragments read once for the QT tiles.  kb / vb: the chunk's fragment
+      // addresses, tb[t]: the bias-table address of the lane's 4 keys (tile 0); ky / kx: their
+      // window row and first column (edge masks, padding)
+      auto chunk = [&](int c, uint32_t kb, uint32_t vb, const uint32_t (&tb)[2], const int (&ky)[2],
+                       const int (&kx)[2]) {
+        const uint4 kf[2] = {lds_ld16(kb), lds_ld16(kb + 1024)};
+        uint4 vt[2];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const uint2 lo = lds_tr8(vb + 512 * dt), hi = lds_tr8(vb + 512 * dt + 1024);
+          vt[dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
         const uint4 one = (K::N % 32 != 0 && c == K::NC - 1) ? one_last : one_full;
+        (void)one;
 #pragma unroll
         for (int j = 0; j < QT; ++j) {
-          const hvk_f32x4 s0 = scores(edge_t, c, 0, j, kf0, ky[0], kx[0]);
-          const hvk_f32x4 s1 = scores(edge_t, c, 1, j, kf1, ky[1], kx[1]);
-          const uint4 pf = make_uint4(
-              hvk_pack2(__builtin_amdgcn_exp2f(s0[0]), __builtin_amdgcn_exp2f(s0[1])),
-              hvk_pack2(__builtin_amdgcn_exp2f(s0[2]), __builtin_amdgcn_exp2f(s0[3])),
-              hvk_pack2(__builtin_amdgcn_exp2f(s1[0]), __builtin_amdgcn_exp2f(s1[1])),
-              hvk_pack2(__builtin_amdgcn_exp2f(s1[2]), __builtin_amdgcn_exp2f(s1[3])));
+          hvk_f32x4 st[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            st[t] = hvk_mfma16(kf[t], qf[j], lds_ld4f(tb[t] - 4u * (uint32_t)(F::DR * j)));
+            if (EDGE) {
+              const int qy = qy0 + (F::DQ / WIN) * j;
+              const int band = ((int)((unsigned)(lim - 1 - qy) >> 31) & erow) |
+                               (((int)((unsigned)(lim - 1 - qx) >> 31) & ecol) << 1);
+              edge_mask<EDGE == 1>(st[t], ky[t], kx[t], band, erow, ecol, lim, mask2);
+            }
+            if (K::N % 32 != 0 && c == K::NC - 1) {
+              const int kp = 32 * c + 16 * t + 4 * gq;
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (kp + r >= K::N) st[t][r] = -INFINITY;
+            }
+          }
+          float p[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[r] = __builtin_amdgcn_exp2f(st[0][r]);
+            p[4 + r] = __builtin_amdgcn_exp2f(st[1][r]);
+          }
+          const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                      hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+#if HVK_FWD_ROWSUM_MFMA
           ls[j] = hvk_mfma16(one, pf, ls[j]);
-          o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
-          o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
+#else
+          ls[j][0] += ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+#endif
+          o[j][0] = hvk_mfma16(vt[0], pf, o[j][0]);
+          o[j][1] = hvk_mfma16(vt[1], pf, o[j][1]);
         }
       };
       if constexpr (F::PER > 0) {
-        // PER chunks span whole window rows: the lane's key rows / columns repeat with it
+        // PER chunks span whole window rows: the lane's key rows / columns repeat with it; the
+        // addresses are laundered once per period (a few base registers, compile-time offsets)
+        constexpr int RPP = 32 * F::PER / WIN;  // window rows per period
 #pragma unroll 1
         for (int cg = 0; cg < K::NC / F::PER; ++cg) {
+          const uint32_t kb = launder(kl + 2048u * F::PER * cg);
+          const uint32_t vb = launder(vl + 2048u * F::PER * cg);
+          const uint32_t tb0 = launder(tl + 4u * RPP * K::R * cg);
+          const int g4 = (int)launder((uint32_t)gq);
 #pragma unroll
           for (int c2 = 0; c2 < F::PER; ++c2) {
             int ky[2], kx[2];
+            uint32_t tb[2];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-              const int kq = 32 * c2 + 16 * t + 4 * gq;  // position inside the period
-              ky[t] = (32 * F::PER / WIN) * cg + kq / WIN;
+              const int kq = 32 * c2 + 16 * t + 4 * g4;  // position inside the period
+              ky[t] = RPP * cg + kq / WIN;
               kx[t] = kq % WIN;
+              tb[t] = tb0 + 4u * (uint32_t)((kq / WIN) * K::R + kq % WIN);
             }
-            chunk(F::PER * cg + c2, ky, kx);
+            chunk(F::PER * cg + c2, kb + 2048u * c2, vb + 2048u * c2, tb, ky, kx);
           }
         }
       } else {
 #pragma unroll 1
         for (int c = 0; c < K::NC; ++c) {
+          const int g4 = (int)launder((uint32_t)gq);
           int ky[2], kx[2];
+          uint32_t tb[2];
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            const int kp = 32 * c + 16 * t + 4 * gq;
+            const int kp = 32 * c + 16 * t + 4 * g4;
             ky[t] = kp / WIN;
             kx[t] = kp - ky[t] * WIN;
+            tb[t] = tl + 4u * (uint32_t)(ky[t] * K::R + kx[t]);
           }
-          chunk(c, ky, kx);
+          chunk(c, launder(kl + 2048u * c), launder(vl + 2048u * c), tb, ky, kx);
         }
-      }
-#pragma unroll
-      for (int j = 0; j < QT; ++j) {
-        float l = ls[j][0];
-        float lshift = 0.f;  // the slow path's row max, on top of M_h
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
-          // slow path (rare, wave-uniform): this tile again with the true running max
-          float m = -INFINITY;
-          l = 0.f;
-          o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
-#pragma unroll 1
-          for (int c = 0; c < K::NC; ++c) {
-            const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
-            const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
-            const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
-            const int kp0 = 32 * c + 4 * gq, kp1 = kp0 + 16;
-            hvk_f32x4 s0 = scores(edge_t, c, 0, j, kf0, kp0 / WIN, kp0 % WIN);
-            hvk_f32x4 s1 = scores(edge_t, c, 1, j, kf1, kp1 / WIN, kp1 % WIN);
-            hvk_settle(s0, s1);
-            float mc = -INFINITY;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s0[r], s1[r]));
-            mc = hvk_group4_max(mc);
-            const float mn = fmaxf(m, mc);
-            const float alpha = __builtin_amdgcn_exp2f(m - mn);
-            m = mn;
-            float p[8];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              p[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
-              p[4 + r] = __builtin_amdgcn_exp2f(s1[r] - mn);
-            }
-            l = l * alpha + ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
-            o[j][0] *= alpha;
-            o[j][1] *= alpha;
-            const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
-                                        hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
-            o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
-            o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
-          }
-          l = hvk_group4_sum(l);
-          lshift = m;
-          hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
-        }
-        // LSE: the query's log2 row constant L2 = M_h + row max + log2(row sum) for the backward
-        if (LSE && gq == 0) a.lse[(size_t)rows[j] * g.nH + h] = Mh + lshift + __log2f(l);
-        const float inv = __builtin_amdgcn_rcpf(l);
-        // accumulator rows: channels 4gq + r (o[0]) and 16 + 4gq + r (o[1]); one permlane swap
-        // per dword gives the lane 8 consecutive channels (one 16-B store)
-        const uint4 pk = hvk_pair_swap(
-            make_uint2(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv), hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv)),
-            make_uint2(hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv), hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv)));
-        hvk_st16(a.out + (size_t)rows[j] * C + h * 32 + hvk_pair_col(gq), pk);
       }
     };
-    if (edge_r || edge_c)
-      run(std::true_type{});
+    if (!(edge_r || edge_c))
+      run(std::integral_constant<int, 0>{});
+    else if ((lim & 3) == 0)
+      run(std::integral_constant<int, 1>{});
     else
-      run(std::false_type{});
+      run(std::integral_constant<int, 2>{});
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+#if HVK_FWD_ROWSUM_MFMA
+      float l = ls[j][0];
+#else
+      float l = hvk_group4_sum(ls[j][0]);
+#endif
+      float lshift = 0.f;  // the slow path's row max, on top of M_h
+      if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(l >= 0x1p-100f)) != 0, 0)) {
+        // slow path (rare, wave-uniform): this tile again with the true running max
+        float m = -INFINITY;
+        l = 0.f;
+        o[j][0] = o[j][1] = hvk_f32x4{0, 0, 0, 0};
+#pragma unroll 1
+        for (int c = 0; c < K::NC; ++c) {
+          const uint4 kf0 = lds16(kimg, fm16(32 * c + li, gq));
+          const uint4 kf1 = lds16(kimg, fm16(32 * c + 16 + li, gq));
+          const uint4 vt0 = tr_frag(vimg, c, 0, li, gq), vt1 = tr_frag(vimg, c, 1, li, gq);
+          const int kp0 = 32 * c + 4 * gq, kp1 = kp0 + 16;
+          hvk_f32x4 s0 = scores(std::integral_constant<int, 0>{}, c, 0, j, kf0, kp0 / WIN, kp0 % WIN);
+          hvk_f32x4 s1 = scores(std::integral_constant<int, 0>{}, c, 1, j, kf1, kp1 / WIN, kp1 % WIN);
+          hvk_settle(s0, s1);
+          if (edge_r || edge_c) {
+            const int qy = qy0 + (F::DQ / WIN) * j;
+            const int band = ((int)((unsigned)(lim - 1 - qy) >> 31) & erow) |
+                             (((int)((unsigned)(lim - 1 - qx) >> 31) & ecol) << 1);
+            edge_mask<false>(s0, kp0 / WIN, kp0 % WIN, band, erow, ecol, lim, mask2);
+            edge_mask<false>(s1, kp1 / WIN, kp1 % WIN, band, erow, ecol, lim, mask2);
+          }
+          float mc = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mc = fmaxf(mc, fmaxf(s0[r], s1[r]));
+          mc = hvk_group4_max(mc);
+          const float mn = fmaxf(m, mc);
+          const float alpha = __builtin_amdgcn_exp2f(m - mn);
+          m = mn;
+          float p[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
+            p[4 + r] = __builtin_amdgcn_exp2f(s1[r] - mn);
+          }
+          l = l * alpha + ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+          o[j][0] *= alpha;
+          o[j][1] *= alpha;
+          const uint4 pf = make_uint4(hvk_pack2(p[0], p[1]), hvk_pack2(p[2], p[3]),
+                                      hvk_pack2(p[4], p[5]), hvk_pack2(p[6], p[7]));
+          o[j][0] = hvk_mfma16(vt0, pf, o[j][0]);
+          o[j][1] = hvk_mfma16(vt1, pf, o[j][1]);
+        }
+        l = hvk_group4_sum(l);
+        lshift = m;
+        hvk_settle(o[j][0], o[j][1]);  // read by the store block this path branches back to
+      }
+      // LSE: the query's log2 row constant L2 = M_h + row max + log2(row sum) for the backward
+      const size_t row = window_token_row(g, b, wh, ww, WIN, qp0 + F::DQ * j);
+      if (LSE && gq == 0) a.lse[row * g.nH + h] = Mh + lshift + __log2f(l);
+      const float inv = __builtin_amdgcn_rcpf(l);
+      // accumulator rows: channels 4gq + r (o[0]) and 16 + 4gq + r (o[1]); one permlane swap
+      // per dword gives the lane 8 consecutive channels (one 16-B store)
+      const uint4 pk = hvk_pair_swap(
+          make_uint2(hvk_pack2(o[j][0][0] * inv, o[j][0][1] * inv), hvk_pack2(o[j][0][2] * inv, o[j][0][3] * inv)),
+          make_uint2(hvk_pack2(o[j][1][0] * inv, o[j][1][1] * inv), hvk_pack2(o[j][1][2] * inv, o[j][1][3] * inv)));
+      hvk_st16(a.out + row * C + h * 32 + hvk_pair_col(gq), pk);
+    }
   }
 }
 
@@ -597,7 +708,6 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     }
     const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
     const bool edge = edge_r || edge_c;
-    load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
 
     // ---------------- phase 1: query tiles qt = wave + WAVES j (positions 16 qt + li)
     struct QIn {
@@ -621,7 +731,10 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       }
       return t;
     };
+    // the first tile's inputs before phase 2's rows: in-order wait counts then never make a
+    // tile wait for the row prefetch (issued next, consumed after the phase)
     QIn cur = load_qt(wave);
+    load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
     for (int qt = wave; qt < K::NT; qt += F::WAVES) {
       QIn nxt = cur;
       if (qt + F::WAVES < K::NT) nxt = load_qt(qt + F::WAVES);
@@ -777,7 +890,6 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     }
     lds_barrier();             // phase-1 reads done; row constants published
     write_rows(sc2);           // q^ scale log2e (exactly the forward's operand), dO
-    if (w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
     lds_barrier();
 
     // ---------------- phase 2: key tiles kt = wave + WAVES j (positions kt + NT li)
@@ -795,6 +907,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       return t;
     };
     KIn kc = load_kt(wave);
+    if (w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
     for (int kt = wave; kt < K::NT; kt += F::WAVES) {
       KIn kn = kc;
       if (kt + F::WAVES < K::NT) kn = load_kt(kt + F::WAVES);
