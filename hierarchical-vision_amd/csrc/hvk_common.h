@@ -61,6 +61,23 @@ void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop);
       return hvk_set_error(HVK_EHIP, "%s: %s", what, hipGetErrorString(e_));     \
   } while (0)
 
+// ---- debug bounds checking (make bounds -> libhvk_bounds.so) ----------------
+// Computed global indices are checked against their extent; a violation is reported by device
+// printf and the index clamped, so the kernel completes instead of faulting the GPU.  The
+// product build compiles the checks away.
+#ifdef HVK_BOUNDS_CHECK
+#define HVK_BCHECK(idx, n) hvk_bcheck((long long)(idx), (long long)(n), __FILE__, __LINE__)
+__device__ __forceinline__ long long hvk_bcheck(long long i, long long n, const char* f, int l) {
+  if (i < 0 || i >= n) {
+    printf("hvk bounds: %s:%d index %lld outside [0, %lld)\n", f, l, i, n);
+    return i < 0 ? 0 : n - 1;
+  }
+  return i;
+}
+#else
+#define HVK_BCHECK(idx, n) (idx)
+#endif
+
 // ---- bf16 <-> f32 ----------------------------------------------------------
 __device__ __forceinline__ float hvk_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hvk_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }

@@ -75,7 +75,9 @@ __global__ __launch_bounds__(256) void mt_ce_fwd_kernel(const float* __restrict_
     loss = lse * tsum - tz;
   } else {
     const int64_t t = tgt[(size_t)b * n_heads + h];
-    loss = lse - z[c0 + (int)t];
+    // a target outside [0, classes) (torch's CE raises "Target out of bounds"): NaN loss, no
+    // out-of-range read
+    loss = (t >= 0 && t < c1 - c0) ? lse - z[c0 + (int)t] : __builtin_nanf("");
   }
   if (lane == 0) {
     row_loss[wid] = loss;
@@ -125,9 +127,15 @@ struct HxeArgs {
 __device__ __forceinline__ void level_range(const HxeArgs& a, int b, int l, int& lo, int& hi) {
   if (l == kLevels - 1) { lo = 0; hi = a.L; return; }
   const int tier = kTiers - 1 - l;
-  const int node = (int)a.tgt[(size_t)b * kTiers + tier];
-  lo = a.nstart[a.tbase[tier] + node];
-  hi = a.nend[a.tbase[tier] + node];
+  const int64_t node = a.tgt[(size_t)b * kTiers + tier];
+  const int n_nodes = tier + 1 < kTiers ? a.tbase[tier + 1] - a.tbase[tier] : a.L;
+  if (node < 0 || node >= n_nodes) {  // out-of-range target: an empty segment (NaN loss), no OOB read
+    lo = 0;
+    hi = -1;
+    return;
+  }
+  lo = a.nstart[a.tbase[tier] + (int)node];
+  hi = a.nend[a.tbase[tier] + (int)node];
 }
 
 __global__ __launch_bounds__(256) void hxe_fwd_kernel(HxeArgs a) {
@@ -147,7 +155,7 @@ __global__ __launch_bounds__(256) void hxe_fwd_kernel(HxeArgs a) {
     Lse tot{sm[0], ss[0]};
     for (int w = 1; w < 4; ++w) tot = lse_merge(tot, Lse{sm[w], ss[w]});
     __syncthreads();
-    const float v = tot.m + __logf(tot.s);
+    const float v = hi < lo ? __builtin_nanf("") : tot.m + __logf(tot.s);  // NaN: target out of range
     loss += a.coeff[l] * v;
     if (threadIdx.x == 0) a.lse[(size_t)b * kLevels + l] = v;
   }

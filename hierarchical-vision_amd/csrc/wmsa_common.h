@@ -34,7 +34,7 @@ __device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh
   int x = ww * win + t % win + g.shift;
   if (y >= g.H) y -= g.H;
   if (x >= g.W) x -= g.W;
-  return (b * g.H + y) * g.W + x;
+  return (int)HVK_BCHECK((b * g.H + y) * g.W + x, (long long)g.B * g.H * g.W);
 }
 
 // L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.

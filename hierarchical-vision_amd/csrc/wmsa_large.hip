@@ -194,7 +194,8 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
       int y = y0 + pos / WIN, x = x0 + pos % WIN;
       if (y >= g.H) y -= g.H;
       if (x >= g.W) x -= g.W;
-      const unsigned voff = (unsigned)(y * g.W + x) * RB + (unsigned)((1 + part) * 2 * C) + lane_col;
+      const unsigned voff = (unsigned)HVK_BCHECK((unsigned)(y * g.W + x) * RB + (unsigned)((1 + part) * 2 * C) + lane_col,
+                                                 IMGB);
       dma16(img, voff, buf + (uint32_t)(part * K::IMG + blk * 1024));
     }
   };

@@ -473,3 +473,24 @@ def test_feature_only_model_forward_head_pre_logits():
     cfg.model.name = "swinv2_tiny_window7_224"
     cfg.model.variant = "linear-probe"
     assert isinstance(models.build_model(cfg, 10), models.FeatureOnlyModel)
+
+
+def test_out_of_range_targets_give_nan_not_oob_reads():
+    """torch's cross-entropy raises on a target outside [0, classes); the kernels flag it with a
+    NaN loss instead of reading outside the logit row (multitask / flat CE and HXE)."""
+    from hvamd.hierarchy import HierarchicalCrossEntropy, MultitaskCrossEntropy, Taxonomy, soft_cross_entropy
+    z = torch.randn(4, 10, device="cuda")
+    assert torch.isnan(soft_cross_entropy(z, torch.tensor([1, 2, 10, 3], device="cuda")))
+    assert torch.isnan(soft_cross_entropy(z, torch.tensor([1, -1, 0, 3], device="cuda")))
+    assert torch.isfinite(soft_cross_entropy(z, torch.tensor([1, 2, 9, 3], device="cuda")))
+    mt = MultitaskCrossEntropy(coeffs=[1.0, 2.0]).cuda()
+    zs = [torch.randn(4, 3, device="cuda"), torch.randn(4, 5, device="cuda")]
+    assert torch.isnan(mt(zs, torch.tensor([[0, 4], [1, 5], [2, 0], [0, 1]], device="cuda")))
+    tax = Taxonomy.synthetic((2, 3, 4, 5, 6, 7, 12))
+    fn = HierarchicalCrossEntropy(tax, tree_weights="exponential").cuda()
+    paths = torch.tensor(tax.leaf_paths[[1, 5]], device="cuda")
+    zl = torch.randn(2, 12, device="cuda")
+    assert torch.isfinite(fn(zl, paths))
+    bad = paths.clone()
+    bad[1, 3] = 99  # tier-3 node id out of range
+    assert torch.isnan(fn(zl, bad))

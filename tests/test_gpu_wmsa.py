@@ -192,3 +192,36 @@ def test_wmsa_large_backward_paths_agree(monkeypatch, B, H, W, nh, win, shift, s
         assert torch.isfinite(a).all(), name
         rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
         assert rel < (3e-2 if name in ("dscale", "dbias") else 1e-2), (name, rel)
+
+def test_bounds_checked_build_reports_no_violation():
+    """The HVK_BOUNDS_CHECK build (make bounds: every W-MSA token row checked against the
+    tensor, violations printed and clamped) runs a shifted w7 and a shifted w24 forward +
+    backward without reporting a violation, and agrees with the product build."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "hierarchical-vision_amd", "libhvk_bounds.so")
+    if not os.path.exists(lib):
+        pytest.skip("libhvk_bounds.so not built (make -C hierarchical-vision_amd/csrc bounds)")
+    code = (
+        "import torch, hvamd.ops as ops\n"
+        "for (H, nh, w, s) in [(14, 2, 7, 3), (48, 2, 24, 12)]:\n"
+        "    g = torch.Generator(device='cuda').manual_seed(0)\n"
+        "    q = torch.randn(2, H * H, 96 * nh, device='cuda', generator=g).bfloat16().requires_grad_(True)\n"
+        "    t = torch.rand(nh, (2 * w - 1) ** 2, device='cuda', generator=g) * 16\n"
+        "    sc = torch.full((nh,), 10.0, device='cuda')\n"
+        "    o = ops.window_attention_core(q, t, sc, H, H, nh, w, s)\n"
+        "    o.float().sum().backward()\n"
+        "    torch.cuda.synchronize()\n"
+        "    print('sum', w, float(o.float().sum()), float(q.grad.float().abs().sum()))\n")
+    out = {}
+    for name, path in (("bounds", lib), ("product", "")):
+        env = dict(os.environ, HVK_LIB_PATH=path) if path else {k: v for k, v in os.environ.items()
+                                                                if k != "HVK_LIB_PATH"}
+        r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "hvk bounds" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-3000:]
+        out[name] = [l for l in r.stdout.splitlines() if l.startswith("sum")]
+    assert out["bounds"] == out["product"], out

@@ -308,3 +308,16 @@ def test_composer_and_swin_checkpoints_round_trip(tmp_path):
         WandbCheckpoint.parse("wandb://a/b/c:v0?x.pt").load_model_dict(str(tmp_path / "empty"))
     with pytest.raises(ValueError):
         parse_checkpoint("s3://bucket/x.pt")
+
+
+def test_host_side_validation_under_asan():
+    """SURVEY.md §5 debug build: libhvk's host code compiled with AddressSanitizer
+    (-Xarch_host -fsanitize=address) and driven by tests/asan/host_checks.cpp through every
+    entry point's argument validation, the workspace / support arithmetic and the error text,
+    without a GPU.  Any ASan report or failed expectation fails the run."""
+    import subprocess
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "hierarchical-vision_amd", "csrc"),
+                        f"-j{min(8, os.cpu_count() or 2)}", "asan"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "host checks ok" in r.stdout
+    assert "AddressSanitizer" not in r.stderr
