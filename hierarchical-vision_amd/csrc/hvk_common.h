@@ -139,6 +139,23 @@ __device__ __forceinline__ void hvk_st16_nt(void* p, uint4 v) {
 __device__ __forceinline__ uint4 hvk_ld16_nt(const void* p) {
   return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const hvk_u32x4*>(p)));
 }
+// Raw buffer access over [base, base + bytes), bytes <= 2^31 (host-checked), built from
+// wave-uniform inputs: a load at offset >= bytes returns 0 and a store there is dropped, so
+// padded lanes take HVK_OOB instead of a branch (an exec branch around a store also makes
+// the compiler's vmcnt accounting conservative: later waits then drain stores in flight).
+#define HVK_OOB 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hvk_rsrc(const void* base, size_t bytes) {
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)bs, 0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
+__device__ __forceinline__ uint4 hvk_bld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void hvk_bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hvk_u32x4, v), r, off, 0, 0);
+}
 __device__ __forceinline__ void hvk_st8(void* p, uint2 v) {
 #ifndef HVK_NT
   *reinterpret_cast<uint2*>(p) = v;

@@ -579,6 +579,457 @@ __global__ __launch_bounds__(kThreads, 1) void wmsa_bwd_kernel(BwdArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Backward, two waves per (window, head) -- a "pair" -- two pairs per 4-wave workgroup, two
+// workgroups per CU: 2 waves per SIMD (<= 256 VGPRs, 72 KB LDS per workgroup), so one wave's
+// MFMA / LDS / exp latency hides under the other's issue, where the one-wave-per-(window,
+// head) kernel above (408 VGPRs, 1 wave per SIMD) stalled on every dependency.
+// Wave hf of a pair owns tiles t = hf + 2j: its query tiles in phase A and its key tiles in
+// phase B.  Per window: own q, k, dO tiles + all V tiles -> registers; q^, k^, dO images of
+// the own rows -> LDS; barrier; all K^ tiles back from LDS; phase A (own query tiles) writes
+// the own rows of the P / scale*dS images; barrier; phase B (own key tiles) reads all rows.
+// Softmax against the head bound M = sc2 + max(bias) folded into the table (no row max;
+// rows whose sum underflows -- a zero query vector -- take the exact-max slow path), and
+// every dS is carried as scale*dS (the dbias / dscale sums are divided by scale once).
+template <int WIN>
+struct PairCfg {
+  using K = WinCfg<WIN>;
+  static constexpr int TPW = (K::NT + 1) / 2;                 // tiles per wave
+  static constexpr int ROWS = 32 * K::NC;                     // padded token rows in LDS images
+  static constexpr int PAIR_LDS = ROWS * 32 * 3 + ROWS * ROWS * 2;  // bf16: q^, k^, dO; P, dS
+  static constexpr size_t LDS = K::TAB * 4 + 16 + 2 * (size_t)PAIR_LDS * 2;
+  static_assert(K::TAB * 4 <= PAIR_LDS * 2, "the dbias reduction reuses one pair's images");
+};
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+  return v;
+}
+
+// build_bias_table with the head bound folded in: tab = bias*log2e - M for real (query, key)
+// pairs, M = sc2 + max bias*log2e over the head (cos <= 1, so every logit - M <= ~0);
+// padded keys -inf, padded queries 0.  Ends with a workgroup barrier.
+template <int WIN>
+__device__ void build_bounded_table(float* tab, float* wmax, const float* __restrict__ src, float sc2) {
+  using K = WinCfg<WIN>;
+  constexpr int PER = K::TAB / kThreads;
+  float v[PER];
+  bool real[PER];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
+    const int qi = blk / K::NT, ki = blk % K::NT;
+    const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
+    real[k] = q < K::N && key < K::N;
+    v[k] = key >= K::N ? -INFINITY : 0.f;
+    if (real[k]) {
+      v[k] = src[(q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1)] * HVK_LOG2E;
+      mx = fmaxf(mx, v[k]);
+    }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  const float M = sc2 + fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+#pragma unroll
+  for (int k = 0; k < PER; ++k) tab[threadIdx.x + k * kThreads] = real[k] ? v[k] - M : v[k];
+  __syncthreads();
+}
+
+#ifdef HVK_STAMPS
+// diagnostic build (tools/bwd_stamps.py): per-phase shader-clock sums over all waves
+__device__ unsigned long long g_bwd_stamps[8];
+#define BSTAMP(k)                                             \
+  do {                                                        \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_prev;                                \
+    st_prev = t_;                                             \
+  } while (0)
+#else
+#define BSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
+template <int WIN>
+__global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
+  using K = WinCfg<WIN>;
+  using PC = PairCfg<WIN>;
+  constexpr int ROWS = PC::ROWS, TPW = PC::TPW, NT = K::NT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WmsaGeom& g = a.g;
+  int chunk, h;
+  if (!decode_item(g, blockIdx.x, chunk, h)) return;
+  int w0, w1;
+  chunk_range(g, chunk, w0, w1);
+  if (w0 >= w1) return;
+
+  // wave-uniform in SGPRs: the window index, its coordinates and edge flags stay scalar
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int pair = wave >> 1, hf = wave & 1;
+  float* btab = reinterpret_cast<float*>(smem);
+  hvk_bf16* const img0 = reinterpret_cast<hvk_bf16*>(smem + K::TAB * 4 + 16);
+  hvk_bf16* qs = img0 + pair * PC::PAIR_LDS;
+  hvk_bf16* ks = qs + ROWS * 32;
+  hvk_bf16* dos = ks + ROWS * 32;
+  hvk_bf16* ps = dos + ROWS * 32;
+  hvk_bf16* dss = ps + ROWS * ROWS;
+  // zero the padded rows of the images once (never rewritten)
+  for (int e = threadIdx.x; e < 2 * PC::PAIR_LDS; e += kThreads) img0[e] = 0;
+  const float scale = a.scale[h];
+  const float sc2 = scale * HVK_LOG2E;
+  build_bounded_table<WIN>(btab, btab + K::TAB, a.bias + (size_t)h * K::R * K::R, sc2);
+
+  const int li = lane & 15, gq = lane >> 4;
+  const int C = g.C, C3 = 3 * g.C;
+  const float mask2 = -100.f * HVK_LOG2E;
+  const uint32_t krow = g.shift ? key_band_bits<WIN>(gq, g.shift, true) : 0u;
+  const uint32_t kcol = g.shift ? key_band_bits<WIN>(gq, g.shift, false) : 0u;
+  const int per_img = g.nWh * g.nWw;
+  // buffer descriptors (launch_bwd splits the batch so each tensor spans < 2^31 bytes):
+  // padded tokens read zeros and drop their stores without a branch
+  const size_t T = (size_t)g.B * g.H * g.W;
+  const auto r_qkv = hvk_rsrc(a.qkv, T * C3 * 2), r_dout = hvk_rsrc(a.dout, T * C * 2);
+  const auto r_dqkv = hvk_rsrc(a.dqkv, T * C3 * 2);
+  // LDS byte offsets as one per-lane base + compile-time immediates (tile t of a 16-row image
+  // = +1024 B; 8-B unit 4dt + u = +512 dt B): few live address registers, no spills
+  const char* const qsb = reinterpret_cast<const char*>(qs);
+  const char* const ksb = reinterpret_cast<const char*>(ks);
+  const char* const dob = reinterpret_cast<const char*>(dos);
+  const int o_row = fm16(li, gq);                       // 16-B unit gq of token row li
+  const int o_r8 = fm8(li, gq);                         // 8-B unit gq of token row li
+  const int o_kt = fm8(4 * gq + (li >> 2), li & 3);     // tr-read of rows 4gq + li/4, unit li&3
+  // P / dS images: row q = 16qi + li, 8-B unit 4ki + gq stored at unit (4ki + gq) ^ f(li)
+  const int fli = ((li ^ (li >> 2)) & 1) | ((li >> 2) & 2) | ((li << 1) & 4);
+  const int o_pw0 = li * ROWS * 2 + ((gq ^ fli) << 3), o_pw1 = li * ROWS * 2 + ((4 ^ gq ^ fli) << 3);
+  // phase B transposed reads: row rq = 4gq + li/4 (+16m + 32c), unit 4kt + (li&3)
+  const int rq0 = 4 * gq + (li >> 2);
+  const int frq = ((rq0 ^ (rq0 >> 2)) & 1) | ((rq0 >> 2) & 2) | ((rq0 << 1) & 4);
+  const int o_trq = fm8(rq0, li & 3);
+
+  hvk_f32x4 dbias[TPW][NT];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int ki = 0; ki < NT; ++ki) dbias[j][ki] = hvk_f32x4{0, 0, 0, 0};
+  float dscale = 0.f;
+  float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+
+  // own q, k, dO tiles and all V tiles of a window -> registers (next window: issued after
+  // phase A into the registers phase A was the last to read, so the loads hide under phase B)
+  uint4 qf[TPW], kf[TPW], df[TPW], vf[NT];
+  int rown[TPW];  // own token rows of the next window, -1 = padding
+  auto load_window = [&](int w) {
+    const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+    // recomputed per window, not hoisted into registers that would spill: a spill reload
+    // here would wait (vmcnt) for every store phase A left in flight
+    int lw = li;
+    asm volatile("" : "+v"(lw));
+    int rt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int tok = 16 * t + lw;
+      rt[t] = tok < K::N ? window_token_row(g, b, wh, ww, WIN, tok) : -1;
+      vf[t] = hvk_bld16(r_qkv, rt[t] < 0 ? HVK_OOB : (uint32_t)(rt[t] * C3 + 2 * C + h * 32 + 8 * gq) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      rown[j] = 2 * j + 1 < NT ? (hf ? rt[2 * j + 1] : rt[2 * j]) : (hf ? -1 : rt[2 * j]);
+      const uint32_t o = rown[j] < 0 ? HVK_OOB : (uint32_t)(rown[j] * C3 + h * 32 + 8 * gq) * 2;
+      const uint32_t od = rown[j] < 0 ? HVK_OOB : (uint32_t)(rown[j] * C + h * 32 + 8 * gq) * 2;
+      qf[j] = hvk_bld16(r_qkv, o);
+      kf[j] = hvk_bld16(r_qkv, o + 2 * C);
+      df[j] = hvk_bld16(r_dout, od);
+    }
+  };
+  // every wave runs the same number of iterations (the barriers are workgroup-wide); a pair
+  // without a window in the last one only joins the barriers
+  const int n_iter = (w1 - w0 + 1) / 2;
+  if (w0 + pair < w1) load_window(w0 + pair);
+  // phase B's dK / dV stores leave at the top of the NEXT iteration, after the waits for the
+  // prefetched loads: in flight behind those loads they would be drained by the waits
+  // (vmcnt counts loads and stores in issue order)
+  uint4 st_k[TPW], st_v[TPW];
+  uint32_t st_off[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    st_k[j] = st_v[j] = make_uint4(0, 0, 0, 0);
+    st_off[j] = HVK_OOB;
+  }
+#ifdef HVK_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
+
+  for (int it = 0; it < n_iter; ++it) {
+    const int w = w0 + 2 * it + pair;
+    const bool act = w < w1;
+    const int rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
+    const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
+    int row[TPW];
+    float rnq[TPW], rnk[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      row[j] = rown[j];
+      const int t = hf + 2 * j;
+      if (act && t < NT) {
+        qf[j] = l2_normalize(qf[j], rnq[j]);
+        kf[j] = l2_normalize(kf[j], rnk[j]);
+        const int o16 = o_row + 1024 * t;
+        *reinterpret_cast<uint4*>((char*)qsb + o16) = qf[j];
+        *reinterpret_cast<uint4*>((char*)ksb + o16) = kf[j];
+        *reinterpret_cast<uint4*>((char*)dob + o16) = df[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      hvk_bst16(r_dqkv, st_off[j], st_k[j]);
+      hvk_bst16(r_dqkv, st_off[j] + 2 * C, st_v[j]);
+    }
+    BSTAMP(0);      // loads landed, normalised, images written
+    lds_barrier();  // the pair's q^, k^, dO images complete
+    BSTAMP(1);
+
+    if (act) {
+      uint4 kfa[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) kfa[t] = *reinterpret_cast<const uint4*>(ksb + o_row + 1024 * t);
+      uint4 kt_frag[K::NC][2];
+#pragma unroll
+      for (int c = 0; c < K::NC; ++c)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const char* b = ksb + o_kt + 2048 * c + 512 * dt;
+          const uint2 lo = hvk_tr_read((const hvk_bf16*)b), hi = hvk_tr_read((const hvk_bf16*)(b + 1024));
+          kt_frag[c][dt] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+
+      // ---------------- phase A: own query tiles, query on the lane
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int qi = hf + 2 * j;
+        if (qi >= NT) break;
+        __builtin_amdgcn_sched_barrier(0);  // one query tile's live set at a time
+        hvk_f32x4 s[NT], dp[NT];
+#pragma unroll
+        for (int ki = 0; ki < NT; ++ki) {
+          s[ki] = hvk_mfma16(kfa[ki], qf[j], hvk_f32x4{0, 0, 0, 0});  // cos(q, k)
+          dp[ki] = hvk_mfma16(vf[ki], df[j], hvk_f32x4{0, 0, 0, 0});  // dO . V
+        }
+        const int q = 16 * qi + li;
+        const float* tq = btab + (qi * NT * 64 + lane) * 4;
+        const uint32_t mm = (edge_r || edge_c) ? mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c) : 0u;
+        float p[NT][4];
+        float sum = 0.f, du = 0.f;
+#pragma unroll
+        for (int ki = 0; ki < NT; ++ki) {
+          const float4 bb = *reinterpret_cast<const float4*>(tq + ki * 256);
+          const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = fmaf(s[ki][r], sc2, bv[r]);
+            if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
+            p[ki][r] = __builtin_amdgcn_exp2f(x);
+            sum += p[ki][r];
+            du = fmaf(p[ki][r], dp[ki][r], du);
+          }
+        }
+        sum = hvk_group4_sum(sum);
+        if (__builtin_expect(__ballot(sum < 0x1p-100f) != 0, 0)) {
+          // a row whose every logit sits far below the head bound (zero query vector):
+          // softmax against the row's own max
+          float mx = -INFINITY;
+#pragma unroll
+          for (int ki = 0; ki < NT; ++ki) {
+            const float4 bb = *reinterpret_cast<const float4*>(tq + ki * 256);
+            const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = fmaf(s[ki][r], sc2, bv[r]);
+              if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
+              p[ki][r] = x;
+              mx = fmaxf(mx, x);
+            }
+          }
+          mx = hvk_group4_max(mx);
+          sum = 0.f;
+          du = 0.f;
+#pragma unroll
+          for (int ki = 0; ki < NT; ++ki)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              p[ki][r] = __builtin_amdgcn_exp2f(p[ki][r] - mx);
+              sum += p[ki][r];
+              du = fmaf(p[ki][r], dp[ki][r], du);
+            }
+          sum = hvk_group4_sum(sum);
+        }
+        du = hvk_group4_sum(du);
+        // P = p/sum, delta = du/sum, scale*dS = p * (dp*(scale/sum) - delta*scale/sum)
+        const float inv = __builtin_amdgcn_rcpf(sum);
+        const float ca = inv * scale, cb = -du * inv * ca;
+        uint32_t dsp[NT][2];
+#pragma unroll
+        for (int ki = 0; ki < NT; ++ki) {
+          float ds[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ds[r] = p[ki][r] * fmaf(dp[ki][r], ca, cb);
+            dbias[j][ki][r] += ds[r];
+            dscale = fmaf(ds[r], s[ki][r], dscale);
+          }
+          dsp[ki][0] = hvk_pack2(ds[0], ds[1]);
+          dsp[ki][1] = hvk_pack2(ds[2], ds[3]);
+          // unit (4ki + gq) ^ f = 4(ki ^ f>>2) + (gq ^ f&3): base 0 / 1 by ki&1, +64 B for ki >= 2
+          const int off = qi * 16 * ROWS * 2 + ((ki & 1) ? o_pw1 : o_pw0) + 64 * (ki >> 1);
+          *reinterpret_cast<uint2*>((char*)ps + off) =
+              make_uint2(hvk_pack2(p[ki][0] * inv, p[ki][1] * inv), hvk_pack2(p[ki][2] * inv, p[ki][3] * inv));
+          *reinterpret_cast<uint2*>((char*)dss + off) = make_uint2(dsp[ki][0], dsp[ki][1]);
+        }
+        // dQ^T = K^T (scale dS^T)
+        hvk_f32x4 dq[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int c = 0; c < K::NC; ++c) {
+          const bool has1 = 2 * c + 1 < NT;
+          const uint4 bf = make_uint4(dsp[2 * c][0], dsp[2 * c][1], has1 ? dsp[2 * c + 1][0] : 0u,
+                                      has1 ? dsp[2 * c + 1][1] : 0u);
+          dq[0] = hvk_mfma16(kt_frag[c][0], bf, dq[0]);
+          dq[1] = hvk_mfma16(kt_frag[c][1], bf, dq[1]);
+        }
+        // normalize backward: dq = (dq^ - q^ (q^ . dq^)) / max(||q||, eps)
+        float qh[2][4], dot = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const uint2 v = *reinterpret_cast<const uint2*>(qsb + o_r8 + 1024 * qi + 512 * dt);
+          qh[dt][0] = hvk_lo(v.x); qh[dt][1] = hvk_hi(v.x);
+          qh[dt][2] = hvk_lo(v.y); qh[dt][3] = hvk_hi(v.y);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dot += qh[dt][r] * dq[dt][r];
+        }
+        dot = hvk_group4_sum(dot);
+        if (rnq[j] >= 1e12f) dot = 0.f;  // ||q|| <= eps: x / eps, no projection term
+        uint2 pk[2];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = (dq[dt][r] - qh[dt][r] * dot) * rnq[j];
+            if (q < K::N) dqb[dt][r] += v[r];
+          }
+          pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+        }
+        const uint4 o = hvk_pair_swap(pk[0], pk[1]);  // all lanes: cross-lane
+        hvk_bst16(r_dqkv, row[j] < 0 ? HVK_OOB : (uint32_t)(row[j] * C3 + h * 32 + hvk_pair_col(gq)) * 2, o);
+      }
+    }
+    BSTAMP(2);
+    if (w + 2 < w1) load_window(w + 2);
+    BSTAMP(3);
+    lds_barrier();  // P / dS images complete
+    BSTAMP(4);
+
+    // ---------------- phase B: own key tiles, key on the lane
+    if (act) {
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const int kt = hf + 2 * j;
+        if (kt >= NT) break;
+        __builtin_amdgcn_sched_barrier(0);
+        hvk_f32x4 dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+        // rows rq0 + 16m + 32c share f(rq0): one base, the rows as immediates
+        const int o_pb = rq0 * ROWS * 2 + ((((4 * kt + (li & 3)) ^ frq) & (ROWS / 4 - 1)) << 3);
+        const char* const psb = reinterpret_cast<const char*>(ps) + o_pb;
+        const char* const dsb = reinterpret_cast<const char*>(dss) + o_pb;
+#pragma unroll
+        for (int c = 0; c < K::NC; ++c) {
+          const int rlo = 32 * c * ROWS * 2, rhi = rlo + 16 * ROWS * 2;
+          uint2 lo = hvk_tr_read((const hvk_bf16*)(psb + rlo)), hi = hvk_tr_read((const hvk_bf16*)(psb + rhi));
+          const uint4 pfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          lo = hvk_tr_read((const hvk_bf16*)(dsb + rlo)); hi = hvk_tr_read((const hvk_bf16*)(dsb + rhi));
+          const uint4 dsfr = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int olo = o_trq + 2048 * c + 512 * dt, ohi = olo + 1024;
+            lo = hvk_tr_read((const hvk_bf16*)(dob + olo)); hi = hvk_tr_read((const hvk_bf16*)(dob + ohi));
+            dv[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), pfr, dv[dt]);
+            lo = hvk_tr_read((const hvk_bf16*)(qsb + olo)); hi = hvk_tr_read((const hvk_bf16*)(qsb + ohi));
+            dk[dt] = hvk_mfma16(make_uint4(lo.x, lo.y, hi.x, hi.y), dsfr, dk[dt]);
+          }
+        }
+        float kh[2][4], dot = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const uint2 v = *reinterpret_cast<const uint2*>(ksb + o_r8 + 1024 * kt + 512 * dt);
+          kh[dt][0] = hvk_lo(v.x); kh[dt][1] = hvk_hi(v.x);
+          kh[dt][2] = hvk_lo(v.y); kh[dt][3] = hvk_hi(v.y);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dot += kh[dt][r] * dk[dt][r];
+        }
+        dot = hvk_group4_sum(dot);
+        if (rnk[j] >= 1e12f) dot = 0.f;
+        uint2 pk[2], pv[2];
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rnk[j];
+          pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+          pv[dt] = make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
+        }
+        st_k[j] = hvk_pair_swap(pk[0], pk[1]);
+        st_v[j] = hvk_pair_swap(pv[0], pv[1]);
+        st_off[j] = row[j] < 0 ? HVK_OOB : (uint32_t)(row[j] * C3 + C + h * 32 + hvk_pair_col(gq)) * 2;
+      }
+    }
+    BSTAMP(5);
+    lds_barrier();  // phase B reads done: the images are free for the next window
+    BSTAMP(6);
+  }
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    hvk_bst16(r_dqkv, st_off[j], st_k[j]);
+    hvk_bst16(r_dqkv, st_off[j] + 2 * C, st_v[j]);
+  }
+#ifdef HVK_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_bwd_stamps[k], st_acc[k]);
+  if (lane == 0) atomicAdd(&g_bwd_stamps[7], 1ull);
+#endif
+
+  // ---- workgroup reduction of the bias / scale gradients (carried as scale*dS), then one
+  // atomic per entry
+  __syncthreads();
+  const float inv_scale = 1.f / scale;
+  float* red = reinterpret_cast<float*>(img0) + pair * (PC::PAIR_LDS / 2);  // pair p's images
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    const int qi = hf + 2 * j;
+    if (qi >= NT) break;
+#pragma unroll
+    for (int ki = 0; ki < NT; ++ki)
+      *reinterpret_cast<float4*>(red + ((qi * NT + ki) * 64 + lane) * 4) =
+          make_float4(dbias[j][ki][0], dbias[j][ki][1], dbias[j][ki][2], dbias[j][ki][3]);
+  }
+  __syncthreads();
+  const float* red0 = reinterpret_cast<const float*>(img0);
+  float* dst = a.dbias_acc + (size_t)h * K::TAB;
+  for (int e = threadIdx.x; e < K::TAB; e += kThreads)
+    atomicAdd(dst + e, (red0[e] + red0[PC::PAIR_LDS / 2 + e]) * inv_scale);
+  dscale = hvk_wave_sum(dscale);
+  if (lane == 0) atomicAdd(a.dscale_acc + h, dscale * inv_scale);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = hvk_row16_sum(dqb[dt][r]);
+      if (li == 0) atomicAdd(a.dqb_acc + h * 32 + 16 * dt + 4 * gq + r, v);
+    }
+}
+
 // Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R], write
 // dscale / dq_bias, and leave the workspace zero for the next call.
 template <int WIN>
@@ -626,6 +1077,15 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
   return HVK_OK;
 }
 
+// HVK_WMSA_BWD_V1=1: the one-wave-per-(window, head) backward (A/B timing only)
+bool bwd_v1() {
+  static const bool v1 = [] {
+    const char* e = getenv("HVK_WMSA_BWD_V1");
+    return e && atoi(e) > 0;
+  }();
+  return v1;
+}
+
 template <int WIN>
 int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, hipStream_t st) {
   const int items = a.g.n_chunks * a.g.nH;
@@ -637,7 +1097,34 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kernel<WIN>, dim3(nblk), dim3(kThreads), lds, st, a);
+  if (bwd_v1()) {
+    HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_kernel<WIN>, dim3(nblk), dim3(kThreads), lds, st, a);
+  } else {
+    constexpr size_t plds = PairCfg<WIN>::LDS;
+    static bool pattr = false;
+    if (!pattr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+      pattr = true;
+    }
+    // buffer descriptors span < 2^31 bytes: launch over batch slices when qkv is larger
+    const size_t img_bytes = (size_t)a.g.H * a.g.W * 3 * a.g.C * 2;
+    const int per = (int)(((size_t)1 << 31) / img_bytes);
+    if (per < 1) return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: one image's qkv exceeds 2 GiB");
+    const size_t tok = (size_t)a.g.H * a.g.W;
+    for (int b0 = 0; b0 < a.g.B; b0 += per) {
+      BwdArgs s = a;
+      s.g.B = a.g.B - b0 < per ? a.g.B - b0 : per;
+      s.g.n_windows = s.g.B * a.g.nWh * a.g.nWw;
+      if (s.g.n_chunks > s.g.n_windows) s.g.n_chunks = s.g.n_windows;
+      s.qkv += b0 * tok * 3 * a.g.C;
+      s.dout += b0 * tok * a.g.C;
+      s.dqkv += b0 * tok * 3 * a.g.C;
+      const int it = s.g.n_chunks * s.g.nH;
+      const int nb = s.g.xcd_runs ? 8 * ((it + 7) / 8) : (s.g.n_chunks + 7) / 8 * 8 * s.g.nH;
+      HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_pair_kernel<WIN>, dim3(nb), dim3(kThreads), plds, st, s);
+    }
+  }
   HVK_CHECK_LAUNCH("wmsa_bwd");
   hipLaunchKernelGGL(wmsa_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dbias_table,
                      dscale, dqb);
@@ -648,6 +1135,15 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
 }  // namespace
 
 extern "C" {
+
+#ifdef HVK_STAMPS
+int hvk_debug_bwd_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamps), 8 * sizeof(unsigned long long)) != hipSuccess)
+    return HVK_EINVAL;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_stamps), z, sizeof(z)) == hipSuccess ? HVK_OK : HVK_EINVAL;
+}
+#endif
 
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
   // [dbias accumulators][dscale nH][dq_bias 32 nH] floats
@@ -734,7 +1230,7 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
     return !e || atoi(e) != 0;
   }();
   if (fill) {
-    int c = 256 / num_heads;
+    int c = (bwd_v1() ? 256 : 512) / num_heads;  // resident workgroups: 1 (v1) or 2 per CU
     if (c < 1) c = 1;
     a.g.n_chunks = c < a.g.n_windows ? c : a.g.n_windows;
     a.g.xcd_runs = 1;

@@ -68,6 +68,13 @@ __device__ __forceinline__ int fm8(int row, int col8) {  // byte offset of 8-B u
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
+// barrier without the vmcnt(0) a __syncthreads() fence adds (prefetched global loads and
+// LDS-DMA stay in flight); LDS writes before it are waited for
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ uint4 lds16(const char* img, int off) {
   return *reinterpret_cast<const uint4*>(img + off);
 }

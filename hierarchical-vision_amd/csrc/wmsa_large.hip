@@ -145,13 +145,6 @@ __device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t 
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
                :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
 }
-// barrier without the vmcnt(0) a __syncthreads() fence adds (the next window's DMA and
-// query loads stay in flight); LDS writes before it are waited for
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 template <int WIN, bool LSE>
 __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_fwd_large_kernel(FwdArgs a) {
