@@ -135,7 +135,7 @@ def wmsa_work(model, batch):
 
 def kernel_names(windows):
     fwd = sorted({f"wmsa_fwd_ring_kernel<{w},HG>" if w <= 8 else f"wmsa_fwd_large_kernel<{w}>" for w in windows})
-    bwd = sorted({f"wmsa_bwd_kernel<{w}>" if w <= 8 else f"wmsa_bwd_large_kernel<{w}>" for w in windows})
+    bwd = sorted({f"wmsa_bwd_pair_kernel<{w}>" if w <= 8 else f"wmsa_bwd_large_kernel<{w}>" for w in windows})
     return "+".join(fwd), "+".join(bwd)
 
 

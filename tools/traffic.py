@@ -1,16 +1,20 @@
 """HBM traffic per launch of the W-MSA kernels from two rocprofv3 PMC passes over a short
 bench.py run (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950):
     python tools/traffic.py FETCH_DIR WRITE_DIR [OUT.json]
-Corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the bytes of 16-B-per-lane
-streaming reads (both W-MSA kernels read by 16-B LDS-DMA / global loads) -> x2; WRITE_SIZE is
-exact for 16-B-per-lane stores.  Both counters are in KiB."""
+Corrections (MI355X_MICROARCH.md, HBM; calibrated on this box class by tools/probe/fetch_calib,
+profiles/round3/fetch_calib.txt): FETCH_SIZE counts half the bytes of coalesced streaming reads
+of 4, 8 and 16 B per lane and of LDS-DMA -> x2; two thirds of them for an isolated 64-B-segment
+shape (x1.5, seg64: segments of one 128-B line fetched as separate requests).  The W-MSA reads
+use x2: at x1.5 the backward's count falls below its algorithmic bytes (impossible for a
+first read), i.e. its segments merge into whole-line requests.  WRITE_SIZE is exact for
+4-16-B stores.  Both counters are in KiB."""
 import collections
 import csv
 import glob
 import json
 import sys
 
-KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_kernel",
+KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_pair_kernel",
            "mlp_fwd": "mlp_fwd_kernel", "mlp_bwd": "mlp_bwd_kernel"}  # the last two: fused stage-0 MLP
 
 
