@@ -68,6 +68,46 @@ __device__ __forceinline__ int fm8(int row, int col8) {  // byte offset of 8-B u
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
+// LDS access through explicit 32-bit LDS addresses (address-space-3 pointers), so a few base
+// registers laundered per loop iteration plus compile-time offsets address every fragment
+typedef __attribute__((address_space(3))) const char lds_cchar;
+__device__ __forceinline__ lds_cchar* lds_ptr(uint32_t a) { return (lds_cchar*)(size_t)a; }
+__device__ __forceinline__ uint4 lds_ld16(uint32_t a) {
+  return __builtin_bit_cast(uint4, *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x4*>(lds_ptr(a)));
+}
+__device__ __forceinline__ hvk_f32x4 lds_ld4f(uint32_t a) {  // 4 consecutive floats (2 x ds_read2_b32)
+  const __attribute__((address_space(3))) float* f = reinterpret_cast<const __attribute__((address_space(3))) float*>(lds_ptr(a));
+  return hvk_f32x4{f[0], f[1], f[2], f[3]};
+}
+__device__ __forceinline__ uint2 lds_tr8(uint32_t a) {
+  hvk_i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) hvk_i16x4*)(lds_ptr(a)));
+  return __builtin_bit_cast(uint2, r);
+}
+__device__ __forceinline__ uint32_t launder(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+__device__ __forceinline__ uint2 lds_ld8(uint32_t a) {
+  return __builtin_bit_cast(uint2, *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x2*>(lds_ptr(a)));
+}
+__device__ __forceinline__ void lds_st16(uint32_t a, uint4 v) {
+  *reinterpret_cast<__attribute__((address_space(3))) hvk_u32x4*>((__attribute__((address_space(3))) char*)(size_t)a) =
+      __builtin_bit_cast(hvk_u32x4, v);
+}
+// LDS-DMA of 16 B per lane (global_load_lds_dwordx4) from inline asm: the compiler does not see
+// it, so it adds no conservative vmcnt(0) before later LDS reads; the caller waits (counted
+// vmcnt) before the barrier that publishes the destination.  base and m0 are wave-uniform.
+__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t m0) {
+  // the base and m0 are wave-uniform: make them scalar for the "s" operands
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+               :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
+}
+
 // barrier without the vmcnt(0) a __syncthreads() fence adds (prefetched global loads and
 // LDS-DMA stay in flight); LDS writes before it are waited for
 __device__ __forceinline__ void lds_barrier() {
@@ -134,6 +174,10 @@ size_t large_acc_floats(int num_heads, int win);  // dbias_acc floats (bins)
 // backward + finalize: dbias_table [nH, R*R], dscale [nH], dq_bias [C] (may be null)
 int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,
               hipStream_t st);
+
+// windows 6 / 7 with an even head count, backward + finalize (wmsa_ring_bwd.hip);
+// HVK_EUNSUPPORTED for any other shape (the caller runs the pair kernel of wmsa.hip)
+int ring_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias, hipStream_t st);
 
 // windows <= 8, forward (wmsa_ring.hip): one persistent workgroup per (window chunk, head
 // group), window slabs staged by LDS-DMA

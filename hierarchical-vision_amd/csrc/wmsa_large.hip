@@ -56,27 +56,6 @@ __device__ __forceinline__ uint4 tr_frag(const char* img, int c, int dt, int li,
   return make_uint4(lo.x, lo.y, hi.x, hi.y);
 }
 
-// LDS access through explicit 32-bit LDS addresses (address-space-3 pointers), so a few base
-// registers laundered per loop iteration plus compile-time offsets address every fragment
-typedef __attribute__((address_space(3))) const char lds_cchar;
-__device__ __forceinline__ lds_cchar* lds_ptr(uint32_t a) { return (lds_cchar*)(size_t)a; }
-__device__ __forceinline__ uint4 lds_ld16(uint32_t a) {
-  return __builtin_bit_cast(uint4, *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x4*>(lds_ptr(a)));
-}
-__device__ __forceinline__ hvk_f32x4 lds_ld4f(uint32_t a) {  // 4 consecutive floats (2 x ds_read2_b32)
-  const __attribute__((address_space(3))) float* f = reinterpret_cast<const __attribute__((address_space(3))) float*>(lds_ptr(a));
-  return hvk_f32x4{f[0], f[1], f[2], f[3]};
-}
-__device__ __forceinline__ uint2 lds_tr8(uint32_t a) {
-  hvk_i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) hvk_i16x4*)(lds_ptr(a)));
-  return __builtin_bit_cast(uint2, r);
-}
-__device__ __forceinline__ uint32_t launder(uint32_t v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
 // The -100 mask of a shifted block's edge window (swinv2.py:357-388, 249-254) on the 4 scores of
 // a lane: its fixed token (band bits `band`: bit 0 = last row band, bit 1 = last column band,
 // each kept only where the window is on that edge: erow / ecol) against 4 consecutive tokens
@@ -137,14 +116,6 @@ struct FCfg {
 // compiler's wait-count pass does not see it, so it never drains it with the vmcnt(0) it puts
 // in front of LDS reads while one of its own LDS-DMAs is pending.  The kernel waits for it with
 // an explicit s_waitcnt before the barrier that publishes the buffer.
-__device__ __forceinline__ void dma16(const void* base, uint32_t voff, uint32_t m0) {
-  // the base and m0 are wave-uniform: make them scalar for the "s" operands
-  const uint64_t b = (uint64_t)base;
-  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
-               :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
-}
 
 template <int WIN, bool LSE>
 __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_fwd_large_kernel(FwdArgs a) {

@@ -96,6 +96,42 @@ __global__ __launch_bounds__(256, 2) void slab(const uint4* __restrict__ qkv, co
   }
 }
 
+// ---- grp: one workgroup per (window chunk, head pair): each token's 128-B pieces of q, k, v
+// and dO for the pair read as contiguous 16-B units; FRAG = 0 writes dq/dk/dv as the same
+// 128-B pieces, FRAG = 1 as the kernels do (16 token rows x 64 B per instruction per head)
+template <int FRAG>
+__global__ __launch_bounds__(256, 2) void grp(const uint4* __restrict__ qkv, const uint4* __restrict__ dout,
+                                              uint4* __restrict__ dqkv, Geom g, int chunks, int D) {
+  const int ng = g.nH / 2;
+  const int gr = blockIdx.x % ng, chunk = blockIdx.x / ng;
+  const int w0 = (int)((long long)chunk * g.nwin / chunks), w1 = (int)((long long)(chunk + 1) * g.nwin / chunks);
+  const int C3u = 3 * g.C / 8, Cu = g.C / 8, go = gr * 8;  // 16-B units
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int w = w0; w < w1; ++w) {
+    // 49 tokens x (3 parts + dO) x 8 units
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    for (int e = threadIdx.x; e < 49 * 32; e += 256) {
+      const int tok = e >> 5, part = (e >> 3) & 3, u = e & 7;
+      const size_t r = token_row(g, w, tok);
+      const uint4 x = part < 3 ? qkv[r * C3u + part * Cu + go + u] : dout[r * Cu + go + u];
+      acc = mix(acc, x, D);
+      if (!FRAG && part < 3) dqkv[r * C3u + part * Cu + go + u] = acc;
+    }
+    if (FRAG) {
+      // 2 heads x 3 parts x 4 tiles of (16 rows x 64 B): one per wave-instruction
+      const int li = lane & 15, gq = lane >> 4;
+      for (int k = wave; k < 24; k += 4) {
+        const int hh = k / 12, part = (k / 4) % 3, t = k % 4;
+        const int tok = 16 * t + li;
+        if (tok < 49) {
+          const size_t r = token_row(g, w, tok);
+          dqkv[r * C3u + part * Cu + go + 4 * hh + gq] = acc;
+        }
+      }
+    }
+  }
+}
+
 // ---- lin: the same bytes as a linear stream
 __global__ __launch_bounds__(256) void lin(const uint4* __restrict__ qkv, const uint4* __restrict__ dout,
                                            uint4* __restrict__ dqkv, size_t n3, int Cu, int C3u) {
@@ -109,6 +145,7 @@ int main(int argc, char** argv) {
   Geom g;
   g.B = 256; g.H = 56; g.W = 56; g.C = 96; g.nH = 3; g.win = 7; g.shift = 3;
   if (argc > 1 && atoi(argv[1]) == 2) { g.H = g.W = 14; g.C = 384; g.nH = 12; }  // stage 2
+  if (argc > 1 && atoi(argv[1]) == 1) { g.H = g.W = 28; g.C = 192; g.nH = 6; }   // stage 1
   g.nWh = g.H / g.win; g.nWw = g.W / g.win; g.nwin = g.B * g.nWh * g.nWw;
   const size_t T = (size_t)g.B * g.H * g.W;
   const size_t qkv_b = T * 3 * g.C * 2, do_b = T * g.C * 2;
@@ -138,6 +175,12 @@ int main(int argc, char** argv) {
     const int chunks = 512 / g.nH;
     snprintf(nm, 80, "pair chunks=%d D=%d", chunks, D);
     run(nm, [&] { hipLaunchKernelGGL(pair, dim3(chunks * g.nH), dim3(256), 0, 0, qkv, dout, dqkv, g, chunks, D); });
+    for (int ch : {256 / (g.nH / 2) * 2, 512 / (g.nH / 2)}) {
+      snprintf(nm, 80, "grp128 store-128B chunks=%d D=%d", ch, D);
+      run(nm, [&] { hipLaunchKernelGGL(grp<0>, dim3(ch * (g.nH / 2)), dim3(256), 0, 0, qkv, dout, dqkv, g, ch, D); });
+      snprintf(nm, 80, "grp128 store-frag chunks=%d D=%d", ch, D);
+      run(nm, [&] { hipLaunchKernelGGL(grp<1>, dim3(ch * (g.nH / 2)), dim3(256), 0, 0, qkv, dout, dqkv, g, ch, D); });
+    }
     for (int ch : {512, 1024, 2048}) {
       snprintf(nm, 80, "slab chunks=%d D=%d", ch, D);
       run(nm, [&] { hipLaunchKernelGGL(slab, dim3(ch), dim3(256), 0, 0, qkv, dout, dqkv, g, ch, D); });
