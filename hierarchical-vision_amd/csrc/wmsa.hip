@@ -1235,10 +1235,6 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
     a.g.n_chunks = c < a.g.n_windows ? c : a.g.n_windows;
     a.g.xcd_runs = 1;
   }
-  if (!bwd_v1()) {
-    const int rc2 = hvk_wmsa::ring_bwd(a, window, dbias_table, dscale, dq_bias, st);
-    if (rc2 != HVK_EUNSUPPORTED) return rc2;
-  }
   switch (window) {
     case 7: return launch_bwd<7>(a, dbias_table, dscale, dq_bias, st);
     case 8: return launch_bwd<8>(a, dbias_table, dscale, dq_bias, st);

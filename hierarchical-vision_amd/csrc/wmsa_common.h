@@ -175,10 +175,6 @@ size_t large_acc_floats(int num_heads, int win);  // dbias_acc floats (bins)
 int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,
               hipStream_t st);
 
-// windows 6 / 7 with an even head count, backward + finalize (wmsa_ring_bwd.hip);
-// HVK_EUNSUPPORTED for any other shape (the caller runs the pair kernel of wmsa.hip)
-int ring_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias, hipStream_t st);
-
 // windows <= 8, forward (wmsa_ring.hip): one persistent workgroup per (window chunk, head
 // group), window slabs staged by LDS-DMA
 int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);

@@ -1,5 +1,5 @@
-// Shared pieces of the LDS-DMA slab W-MSA kernels for windows <= 8 (wmsa_ring.hip: forward,
-// wmsa_ring_bwd.hip: backward): slab geometry, inline-asm LDS reads, compact bias gathers.
+// Shared pieces of the LDS-DMA slab W-MSA forward for windows <= 8 (wmsa_ring.hip):
+// slab geometry, inline-asm LDS reads, compact bias gathers.
 #pragma once
 #include "wmsa_common.h"
 

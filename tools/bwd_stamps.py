@@ -13,14 +13,12 @@ from tools.bench_wmsa import STAGES  # noqa: E402
 
 PHASES = ["top: loads + normalise + image writes", "barrier 1", "K^ reads + phase A",
           "next-window load issue", "barrier 2", "phase B", "barrier 3"]
-RING_PHASES = ["slab wait (vmcnt)", "top barrier", "deferred stores + DMA issue", "normalise in place",
-               "barriers 1 + 2", "K^/V reads + phase A", "phase B"]
+
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stage", type=int, default=0)
-    ap.add_argument("--ring", action="store_true", help="the ring (slab) kernel's stamps")
     a = ap.parse_args()
     from hvamd import _lib, ops
     name, B, H, W, C, nh, win, shift, _ = STAGES[a.stage]
@@ -33,15 +31,14 @@ def main():
     for it in range(3):
         out = ops.window_attention_core(qkv, tab, scale, H, W, nh, win, shift)
         torch.cuda.synchronize()
-        rd = lib.hvk_debug_ring_bwd_stamps if a.ring else lib.hvk_debug_bwd_stamps
-        rd(buf)  # clear
+        lib.hvk_debug_bwd_stamps(buf)  # clear
         out.backward(g)
         torch.cuda.synchronize()
-        rd(buf)
+        lib.hvk_debug_bwd_stamps(buf)
     tot = sum(buf[:7])
     waves = buf[7]
     print(f"{name}: {waves} waves, {tot / waves:.0f} cycles per wave in the window loop")
-    for k, p in enumerate(RING_PHASES if a.ring else PHASES):
+    for k, p in enumerate(PHASES):
         print(f"  {p:40s} {buf[k] / waves:10.0f} cyc/wave  {100 * buf[k] / tot:5.1f} %")
 
 
