@@ -32,6 +32,10 @@ sys.path.insert(0, ROOT)
 METRIC = "images/sec/GPU SwinV2-T 224² HXE bs256; W-MSA HBM GB/s vs peak; 1→8 scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 MFMA_PEAK_TFS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
+# transcendental roof: v_exp_f32 issues at 8 cycles per wave64 instruction on a SIMD (quarter
+# of the 2-cycle VALU rate; MI355X_MICROARCH.md, vector-instruction issue cost): 8 exp per
+# cycle per SIMD x 1024 SIMDs x 2.4 GHz
+EXP_PEAK_TS = 8 * 1024 * 2.4e9 / 1e12
 
 
 def parse():
@@ -117,9 +121,11 @@ def wmsa_work(model, batch):
     """Per-step algorithmic work of the W-MSA kernels, summed over blocks with
     each block's effective window: bytes forward 8*T*C (bf16 qkv read 3C + out write C per
     token), backward 16*T*C; flops forward 4*T*N*C (Q K^T and P V), backward 10*T*N*C, with
-    T = batch*H*W tokens and N = w*w tokens per window."""
+    T = batch*H*W tokens and N = w*w tokens per window; exponentials forward T*N*nH (one per
+    query-key pair and head), backward 2*T*N*nH (P recomputed in the query phase and again in
+    the key phase of the large-window kernels), nH = C/32."""
     from hvamd.swinv2 import SwinTransformerBlock
-    w = dict(fwd_bytes=0, bwd_bytes=0, fwd_flops=0, bwd_flops=0, windows=set())
+    w = dict(fwd_bytes=0, bwd_bytes=0, fwd_flops=0, bwd_flops=0, fwd_exp=0, bwd_exp=0, windows=set())
     for m in model.modules():
         if isinstance(m, SwinTransformerBlock):
             H, W = m.input_resolution
@@ -129,6 +135,8 @@ def wmsa_work(model, batch):
             w["bwd_bytes"] += 16 * tc
             w["fwd_flops"] += 4 * tc * n
             w["bwd_flops"] += 10 * tc * n
+            w["fwd_exp"] += tc * n // 32
+            w["bwd_exp"] += 2 * tc * n // 32
             w["windows"].add(m.window_size)
     return w
 
@@ -139,7 +147,7 @@ def kernel_names(windows):
     return "+".join(fwd), "+".join(bwd)
 
 
-def roofline_block(kernel, nbytes, flops, ms_total, launches, steps, traffic):
+def roofline_block(kernel, nbytes, flops, ms_total, launches, steps, traffic, n_exp=None):
     """The kernel's achieved HBM rate and MFMA rate against the MI355X peaks; bound = the
     roof its arithmetic intensity sits under (ridge = 2.5 PF / 8 TB/s = 312 flop/B)."""
     sec = ms_total / 1000.0
@@ -160,7 +168,12 @@ def roofline_block(kernel, nbytes, flops, ms_total, launches, steps, traffic):
             "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "achieved_tflops": round(tfs, 1),
             "mfma_frac": round(tfs / MFMA_PEAK_TFS, 4),
             "avg_launch_us": round(1000 * ms_total / launches, 2),
-            "ms_per_step": round(ms_total / steps, 3)}
+            "ms_per_step": round(ms_total / steps, 3),
+            # third roof for the large-window kernels, whose softmax is exp-issue heavy
+            **({"trans": {"exp_per_step": n_exp, "achieved": round(n_exp * steps / sec / 1e12, 3),
+                          "peak": round(EXP_PEAK_TS, 3), "unit": "Texp/s",
+                          "frac": round(n_exp * steps / sec / 1e12 / EXP_PEAK_TS, 4)}}
+               if n_exp else {})}
 
 
 def cpu_model():
@@ -354,8 +367,10 @@ def main():
         bw_ms, bw_n, _ = timer["wmsa_bwd"]
         n_launch = fw_n // timed_steps
         traffic = measured_traffic("wmsa_fwd") if default_cfg else None
+        large = max(work["windows"]) > 8
         r = roofline_block(f"{kf} (all {n_launch} launches per step)", work["fwd_bytes"],
-                           work["fwd_flops"], fw_ms, fw_n, timed_steps, traffic)
+                           work["fwd_flops"], fw_ms, fw_n, timed_steps, traffic,
+                           work["fwd_exp"] if large else None)
         r["timing"] = ("dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps just "
                        "before the graph capture (replays carry no per-kernel events)" % timed_steps
                        if args.graph else
@@ -366,7 +381,7 @@ def main():
         result["roofline"] = r
         result["roofline_bwd"] = roofline_block(
             kb, work["bwd_bytes"], work["bwd_flops"], bw_ms, bw_n, timed_steps,
-            measured_traffic("wmsa_bwd") if default_cfg else None)
+            measured_traffic("wmsa_bwd") if default_cfg else None, work["bwd_exp"] if large else None)
         # dense contractions on libhvk's MFMA GEMMs (every Linear but the classifier head):
         # their algorithmic flops (2 M N K per launch, summed by the library) over their
         # dispatch-packet-timed durations

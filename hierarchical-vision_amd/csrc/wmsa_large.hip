@@ -917,7 +917,8 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
           }
           // CPB-table gradient: this wave's own bins, batches of BATCH elements that never share a
           // bin across the lanes (strided key tiles); the compiler fences keep one batch's reads
-          // behind the previous batch's writes
+          // behind the previous batch's writes.  (LDS float atomics instead -- ds_add_f32, one op
+          // per element -- ran the w24 backward 4.9x slower: profiles/round3/large_bins_atomic_ab.txt)
 #pragma unroll
           for (int b0 = 0; b0 < 8; b0 += F::BATCH) {
             float v[F::BATCH];
