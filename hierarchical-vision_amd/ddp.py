@@ -4,14 +4,19 @@ gets it implicitly from composer's DDP wrapper, main.py:104-124).
 
 Design for MI355X:
 * Gradients live in a few large flat f32 buffers ("buckets"), one per ~`bucket_mb`
-  of parameters in reverse registration order (= roughly backward order); every
-  ``param.grad`` is a view into its bucket, so there is no pack / unpack copy.
-* A post-accumulate-grad hook counts arrivals; when a bucket's last gradient is
-  accumulated the bucket's all-reduce is enqueued immediately (RCCL runs it on
-  its own HIP stream, ordered after the producing kernels), so communication of
-  late layers overlaps the backward of early ones.  Buckets are big (default
-  64 MB): xGMI is point-to-point (7 links/GPU) and RCCL's ring/tree per-call
-  cost is amortised only by large messages.
+  of parameters in reverse registration order (= roughly backward order), the first
+  (last layers: head, stage 3) only ~`first_mb` so the first all-reduce starts early;
+  after the exchange every ``param.grad`` is a view into its bucket (the optimizer and
+  the clip read the buckets, no pack / unpack copy).
+* Between steps ``param.grad`` is None, so autograd hands each fresh weight gradient over
+  without a ``grad += new`` pass (and the buckets need no per-step zero_); the
+  post-accumulate-grad hook copies it into its bucket view (one read + one write of the
+  gradient instead of zero + read-add-write) and counts arrivals: when a bucket's last
+  gradient is in, the bucket's all-reduce is enqueued immediately (RCCL runs it on its
+  own HIP stream, ordered after the producing kernels), so communication of late layers
+  overlaps the backward of early ones.  Later buckets are big (default 64 MB): xGMI is
+  point-to-point (7 links/GPU) and RCCL's ring/tree per-call cost is amortised only by
+  large messages.
 * ``synchronize()`` waits for all buckets (makes the current stream wait on the
   RCCL stream, no host sync).  The 1/world mean is not a separate pass over the 141 MB: the
   trainer hands it to the fused optimizer step as a gradient scale (optim.DecoupledSGDW);
@@ -23,7 +28,8 @@ import torch.distributed as dist
 
 
 class GradientBuckets:
-    def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None):
+    def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
+                 first_mb: float = 8.0):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         params = [p for p in module.parameters() if p.requires_grad]
@@ -35,10 +41,12 @@ class GradientBuckets:
         if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
             return
         limit = int(bucket_mb * 1024 * 1024 / 4)
+        first = int(min(first_mb, bucket_mb) * 1024 * 1024 / 4)
         self.buckets = []  # list of (flat buffer, [params])
+        self._view = {}    # param -> its view in the bucket
         cur, size = [], 0
         for p in reversed(params):
-            if cur and size + p.numel() > limit:
+            if cur and size + p.numel() > (first if not self.buckets else limit):
                 self.buckets.append(self._make(cur, size))
                 cur, size = [], 0
             cur.append(p)
@@ -52,20 +60,23 @@ class GradientBuckets:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
         self.reset()
 
-    @staticmethod
-    def _make(params, n):
+    def _make(self, params, n):
         dev = params[0].device
         flat = torch.zeros(n, device=dev, dtype=torch.float32)
         off = 0
         for p in params:
             if p.dtype != torch.float32:
                 raise TypeError("master parameters must be f32")
-            p.grad = flat[off:off + p.numel()].view_as(p)
+            self._view[p] = flat[off:off + p.numel()].view_as(p)
             off += p.numel()
         return flat, params
 
     def _make_hook(self, bi):
         def hook(p):
+            v = self._view[p]
+            if p.grad is not v:  # the fresh gradient autograd handed over -> its bucket slot
+                v.copy_(p.grad)
+                p.grad = v
             self._pending[bi] -= 1
             if self._pending[bi] == 0 and self.enabled and not self.defer:
                 flat = self.buckets[bi][0]
@@ -74,20 +85,26 @@ class GradientBuckets:
         return hook
 
     def reset(self):
-        """Zero every bucket in place (grads stay views) before the next backward."""
+        """Before the next backward: every param.grad None (autograd hands the new gradient
+        over; the hook copies it into the bucket), arrival counts re-armed.  No zero pass."""
+        for p in self.params:
+            p.grad = None
         if not self.enabled:
-            for p in self.params:
-                p.grad = None
             return
         for i, (flat, ps) in enumerate(self.buckets):
-            flat.zero_()
             self._pending[i] = len(ps)
             self._works[i] = None
-            for p in ps:  # re-attach if an optimizer set .grad = None
-                if p.grad is None or p.grad.data_ptr() < flat.data_ptr() or \
-                        p.grad.data_ptr() >= flat.data_ptr() + flat.numel() * 4:
-                    raise RuntimeError("param.grad was detached from its bucket; "
-                                       "use zero_grad(set_to_none=False) or buckets.reset()")
+
+    def _fill_missing(self, i):
+        """Parameters of bucket i that got no gradient this backward: zero slots."""
+        for p in self.buckets[i][1]:
+            v = self._view[p]
+            if p.grad is not v:
+                if p.grad is None:
+                    v.zero_()
+                else:
+                    v.copy_(p.grad)
+                p.grad = v
 
     def synchronize(self, scale=True):
         """Wait for every bucket's all-reduce; with scale, turn the sums into means in place
@@ -96,20 +113,24 @@ class GradientBuckets:
             return
         for i, (flat, _) in enumerate(self.buckets):
             w = self._works[i]
-            if w is None:  # a bucket whose grads never arrived (unused params): reduce now
+            if w is None:  # a bucket whose grads never all arrived (unused params): reduce now
+                self._fill_missing(i)
                 w = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
             w.wait()
             if scale:
                 flat.div_(self.world)
 
     def zero_(self):
-        """Zero the buckets in place (graph mode: captured at the start of the backward graph)."""
+        """Zero the buckets in place (graph mode: captured at the start of the backward graph,
+        which the gradients of that capture then overwrite or add to)."""
         for flat, _ in self.buckets:
             flat.zero_()
 
     def allreduce_now(self):
         """Graph mode: all-reduce every bucket (SUM) between the backward and optimizer graph
         replays, eagerly (RCCL is not captured); the mean is taken inside the optimizer graph."""
+        for i in range(len(self.buckets)):
+            self._fill_missing(i)
         works = [dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
                  for flat, _ in self.buckets]
         for w in works:

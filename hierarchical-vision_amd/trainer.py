@@ -111,9 +111,9 @@ class Trainer:
         self.state.outputs = self.state.loss = None
         torch.cuda.synchronize()
         self.buckets.defer = True
-        if not self.buckets.enabled:
-            for p in self.model.parameters():
-                p.grad = None  # allocated inside the graph's pool, kept across replays
+        # gradients allocated inside the graph's pool, kept across replays (with buckets the
+        # hooks copy them into the bucket views and leave .grad = view)
+        self.buckets.reset()
         self._g_bwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_bwd):
             self._g_loss = self._forward_backward(batch)

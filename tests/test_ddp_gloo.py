@@ -61,6 +61,46 @@ def test_bucketed_allreduce_equals_full_batch_gradient():
             assert torch.allclose(torch.from_numpy(g), p.grad, atol=1e-6), r
 
 
+def _worker_views(rank, world, port, out):
+    """After the exchange every grad is a view into its bucket (the optimizer's flat
+    buffers), a parameter that got no gradient reads zeros, the first bucket is the small
+    one, and between steps .grad is None (autograd hands the new gradient over: no
+    grad += new, no zero pass)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hvamd.ddp import GradientBuckets
+    net = _net()
+    net.unused = torch.nn.Parameter(torch.ones(5))
+    buckets = GradientBuckets(net, bucket_mb=0.004, first_mb=0.0005)
+    sizes = [b[0].numel() for b in buckets.buckets]
+    res = {"first_small": sizes[0] <= 0.0005 * 2 ** 18 + 32 * 32 and sizes[0] < max(sizes)}
+    x, y = _data()
+    res["none_before"] = all(p.grad is None for p in net.parameters())
+    ok_views, unused_zero = True, True
+    for step in range(2):
+        torch.nn.functional.cross_entropy(net(x[rank * 4:rank * 4 + 4]), y[rank * 4:rank * 4 + 4]).backward()
+        buckets.synchronize()
+        flats = buckets.flat_buffers()
+        for p in net.parameters():
+            base = p.grad.data_ptr()
+            ok_views &= any(f.data_ptr() <= base < f.data_ptr() + 4 * f.numel() for f in flats)
+        unused_zero &= bool((net.unused.grad == 0).all())
+        buckets.reset()
+        res["none_after_reset"] = all(p.grad is None for p in net.parameters())
+    res["views"] = ok_views
+    res["unused_zero"] = unused_zero
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_bucket_views_unused_params_small_first_bucket():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker_views, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert all(out[r].values()), out[r]
+
+
 # ---------------------------------------------------------------- the real Trainer, world 2
 MINI = dict(img_size=56, embed_dim=32, depths=(2, 2), num_heads=(1, 2), window_size=7)
 TAX_SIZES = (2, 3, 4, 5, 6, 7, 12)

@@ -53,9 +53,16 @@ def _run(rank, world, port, out, steps=2):
     for _ in range(steps):
         trainer.train_step((x[sl], y[sl]))
     torch.cuda.synchronize()
+    # one more step under the profiler: the elementwise adds it launches (gradient sums)
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        trainer.train_step((x[sl], y[sl]))
+        torch.cuda.synchronize()
+    adds = sum(1 for e in prof.events() if "CUDAFunctor_add" in e.name)
     # what the steps moved: the update (and the EMA's pull) itself, not the weights around it
     out[rank] = ([(p.detach() - q).cpu().numpy() for p, q in zip(model.parameters(), p0)],
-                 [(e - q).cpu().numpy() for e, q in zip(ema.ema_params, p0)], opt._fused is not None)
+                 [(e - q).cpu().numpy() for e, q in zip(ema.ema_params, p0)], opt._fused is not None,
+                 adds)
     if world > 1:
         dist.destroy_process_group()
 
@@ -67,6 +74,10 @@ def test_two_ranks_equal_one_process_full_batch():
     single = {}
     _run(0, 1, 0, single)
     assert out[0][2] and single[0][2]  # the fused optimizer step ran on both sides
+    # the bucketed exchange adds no gradient pass: autograd hands each weight gradient over
+    # (.grad is None between steps) and the hook copies it into the bucket -- the elementwise
+    # adds of a world-2 step are the model's own (e.g. proj.weight's two contributions)
+    assert out[0][3] == single[0][3] and out[1][3] == single[0][3], (out[0][3], out[1][3], single[0][3])
     # parameter and EMA deltas over the two steps; per-rank weight-gradient reductions run over
     # half the tokens (another chunking) and the backward's bias-table atomics sum in a
     # run-dependent order: 2e-2 per tensor bounds it (a missing 1/world would be 100 %)
