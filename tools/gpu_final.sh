@@ -22,3 +22,7 @@ if [ -z "$NO_PROF" ]; then
   bash tools/gpu_traffic.sh > /dev/null || exit 1
   cat gpurun_out/traffic/bench_traffic.json
 fi
+if [ -z "$NO_PROF" ]; then
+  bash tools/gpu_mfma_pmc.sh > /dev/null || exit 1
+  cat gpurun_out/mfma_pmc/mfma_pmc.json | head -c 3000
+fi
