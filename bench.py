@@ -62,7 +62,7 @@ def parse():
 
 def build(args, device):
     from hvamd import configs, hierarchy, models, optim
-    from hvamd.algorithmic import GradientClipping
+    from hvamd.algorithmic import EMA, GradientClipping
     from hvamd.trainer import Trainer
 
     cfg = configs.Config()
@@ -84,7 +84,9 @@ def build(args, device):
     cfg.optim.lr = 0.02
     model = models.build_composer_model(cfg, info).to(device)
     opt = optim.build_optimizer(cfg, model)
-    trainer = Trainer(model, opt, [GradientClipping("norm", 2.0)])
+    # the recipe's EMA (configs/pretrain/inat21.yaml:32-35: half-life 100 batches, updated every
+    # 20), folded into the fused optimizer step on its update batches
+    trainer = Trainer(model, opt, [GradientClipping("norm", 2.0), EMA(half_life="100ba", update_interval="20ba")])
     return cfg, tax, model, trainer
 
 
