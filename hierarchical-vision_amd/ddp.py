@@ -29,12 +29,14 @@ import torch.distributed as dist
 
 class GradientBuckets:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
-                 first_mb: float = 8.0):
+                 first_mb: float = 8.0, force: bool = False):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         params = [p for p in module.parameters() if p.requires_grad]
         self.params = params
-        self.enabled = self.world > 1
+        # force: exchange even at world 1 (a one-rank RCCL group exercises the whole hook /
+        # all-reduce / synchronize path on a one-GPU box, tests/test_gpu_ddp.py)
+        self.enabled = self.world > 1 or (force and dist.is_initialized())
         self.defer = False  # graph mode: no hook-launched all-reduce (allreduce_now() instead)
         self.buckets = []
         self._hooks = []

@@ -86,3 +86,49 @@ def test_two_ranks_equal_one_process_full_batch():
             a, b = torch.from_numpy(a), torch.from_numpy(b)
             rel = ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
             assert rel < 2e-2, (r, rel)
+
+
+def test_rccl_one_rank_buckets_match_plain_step():
+    """The RCCL (nccl backend) path on hardware: a one-rank process group with the buckets
+    forced on runs the hook-launched all-reduces on RCCL's stream, synchronize() and the
+    fused step on the bucket views; with one rank the exchange is the identity, so two steps
+    must equal two steps without buckets up to the run-to-run order of the backward's
+    bias-table atomics (1e-4 relative per tensor; a lost, doubled or stale gradient is O(1))."""
+    from hvamd import hierarchy, models, optim, swinv2
+    from hvamd.algorithmic import GradientClipping
+    from hvamd.ddp import GradientBuckets
+    from hvamd.trainer import Trainer
+    dev = torch.device("cuda:0")
+
+    def run(bucketed):
+        torch.manual_seed(0)
+        tax = hierarchy.Taxonomy.synthetic(TAX_SIZES)
+        net = swinv2.SwinTransformerV2(img_size=56, embed_dim=32, depths=[2, 2], num_heads=[1, 2],
+                                       window_size=7, num_classes=tax.num_leaves,
+                                       drop_path_rate=0.0).to(dev)
+        loss_fn = hierarchy.HierarchicalCrossEntropy(tax, tree_weights="exponential").to(dev)
+        model = models.Model(net, None, None, loss_fn)
+        opt = optim.DecoupledSGDW(optim.set_weight_decay(model), lr=0.05, momentum=0.9,
+                                  weight_decay=5e-4)
+        trainer = Trainer(model, opt, [GradientClipping("norm", 1e4)])
+        if bucketed:
+            trainer.buckets = GradientBuckets(model, bucket_mb=0.05, force=True)
+            assert trainer.buckets.enabled and len(trainer.buckets.buckets) > 2
+        g = torch.Generator(device=dev).manual_seed(1)
+        x = torch.randn(4, 3, 56, 56, device=dev, generator=g)
+        y = torch.tensor(tax.leaf_paths[[1, 5, 9, 11]], device=dev)
+        for _ in range(2):
+            trainer.train_step((x, y))
+        torch.cuda.synchronize()
+        return [p.detach().cpu().clone() for p in model.parameters()]
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        a = run(True)
+    finally:
+        dist.destroy_process_group()
+    b = run(False)
+    for u, v in zip(a, b):
+        rel = ((u - v).norm() / v.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-4, rel
