@@ -81,37 +81,46 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     for (int e = threadIdx.x; e < BN; e += kThreads) bl[e] = bias[n0 + e];
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  // wave-uniform tile index: every global access goes through a buffer view of its 16-row
+  // tile clipped at M (hvk_tile_rsrc), so rows past M need no exec branch -- a load or store
+  // under a branch made the compiler's vmcnt accounting conservative: it waited vmcnt(0) at
+  // every tile's MFMAs, for the tile-ahead prefetch and every store in flight
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tiles = (M + 15) >> 4;
   const int stride = row_groups * WAVES;
   int tile = rg * WAVES + wave;
 
   auto load_x = [&](int t, uint4 (&xf)[G::KS]) {
-    const int row = 16 * t + li;
-    const bool ok = t < tiles && row < M;
-    const hvk_bf16* xp = X + (size_t)row * K + 8 * g;
+    const auto rx = hvk_tile_rsrc(X, 16 * t, M, K * 2);
+    const uint32_t o = (uint32_t)(li * K + 8 * g) * 2;
 #pragma unroll
     for (int s = 0; s < G::KS; ++s) {
       const bool in_k = (K % 32 == 0) || s + 1 < G::KS || g < 2;
-      xf[s] = (ok && in_k) ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+      xf[s] = hvk_bld16(rx, in_k ? o + 64 * s : HVK_OOB);
     }
   };
 
   // EPI 2: the saved pre-activation of the row tile, prefetched one tile ahead like X
   auto load_h = [&](int t, uint4 (&hf)[EPI == 2 ? G::NT / 2 : 1]) {
     if (EPI != 2) return;
-    const int row = 16 * t + li;
-    const bool ok = t < tiles && row < M;
+    const auto rh = hvk_tile_rsrc(Y2, 16 * t, M, N * 2);
+    const uint32_t o = (uint32_t)(li * N + n0 + 8 * g) * 2;
 #pragma unroll
     for (int j = 0; j < G::NT / 2; ++j)
-      hf[j] = ok ? ((HVK_NT_SAVED & 8) ? hvk_ld16_nt(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j)
-                                       : hvk_ld16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j))
-                 : make_uint4(0, 0, 0, 0);
+      hf[j] = (HVK_NT_SAVED & 8) ? hvk_bld16_nt(rh, o + 64 * j) : hvk_bld16(rh, o + 64 * j);
   };
   uint4 xf[G::KS];
   load_x(tile, xf);
   uint4 hf[EPI == 2 ? G::NT / 2 : 1];
   load_h(tile, hf);
+  // the first tile's operands land before the loop (the loop header's wait then serves only
+  // the back edge, counted, instead of vmcnt(0) on every iteration)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) hvk_launder(xf[s]);
+  if (EPI == 2)
+#pragma unroll
+    for (int j = 0; j < (EPI == 2 ? G::NT / 2 : 1); ++j) hvk_launder(hf[j]);
   float cs[EPI == 2 ? G::NT / 2 : 1][8];
   if (EPI == 2)
 #pragma unroll
@@ -126,6 +135,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     if (PREF) load_x(tile + stride, xn);
     uint4 hn[EPI == 2 ? G::NT / 2 : 1];
     load_h(tile + stride, hn);
+    __builtin_amdgcn_sched_barrier(0);  // the next tile's loads issue here, not after the MFMAs
     hvk_f32x4 acc[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
@@ -137,9 +147,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
 #pragma unroll
       for (int t = 0; t < G::NT; ++t)
         acc[t] = hvk_mfma16(wl[(t * G::U4 + 4 * s + g) * 16 + li], xg[s], acc[t]);
-    const int row = 16 * tile + li;
-    if (row < M) {
-      hvk_bf16* yp = Y + (size_t)row * N + n0 + 8 * g;
+    {
+      const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N * 2);
+      const auto ry2 = hvk_tile_rsrc(Y2, 16 * tile, M, N * 2);
+      const uint32_t yo = (uint32_t)(li * N + n0 + 8 * g) * 2;
 #pragma unroll
       for (int j = 0; j < G::NT / 2; ++j) {
         float v[8];
@@ -158,9 +169,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             v[e + 1] *= d.y;
           }
           const uint4 gv = hvk_pack8(v);
-          hvk_st16(yp + 32 * j, gv);
+          hvk_bst16(ry, yo + 64 * j, gv);
           float r[8];
-          hvk_unpack8(gv, r);  // the bias gradient sums the stored (rounded) gradient
+          hvk_unpack8(gv, r);  // the bias gradient sums the stored (rounded) gradient (0 past M)
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[j][e] += r[e];
           continue;
@@ -173,9 +184,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
         }
         const uint4 hv = hvk_pack8(v);
         if (EPI == 1 && (HVK_NT_SAVED & 1))
-          hvk_st16_nt(yp + 32 * j, hv);
+          hvk_bst16_nt(ry, yo + 64 * j, hv);
         else
-          hvk_st16(yp + 32 * j, hv);
+          hvk_bst16(ry, yo + 64 * j, hv);
         if (EPI == 1) {
           float u[8];
           hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             u[e] = y.x;
             u[e + 1] = y.y;
           }
-          hvk_st16(Y2 + (size_t)row * N + n0 + 8 * g + 32 * j, hvk_pack8(u));
+          hvk_bst16(ry2, yo + 64 * j, hvk_pack8(u));
         }
       }
     }
@@ -254,23 +265,32 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
   for (int e = threadIdx.x; e < N2; e += kThreads) b2l[e] = b2 ? b2[e] : 0.f;
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  // branch-free global accesses through 16-row tile buffer views (see linear_kernel)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tiles = (M + 15) >> 4;
   const int stride = row_groups * WAVES;
   int tile = blockIdx.x * WAVES + wave;
   auto load_x = [&](int t, uint4 (&xf)[G1::KS]) {
-    const int row = 16 * t + li;
-    const bool ok = t < tiles && row < M;
-    const hvk_bf16* xp = X + (size_t)row * K + 8 * g;
+    const auto rx = hvk_tile_rsrc(X, 16 * t, M, K * 2);
+    const uint32_t o = (uint32_t)(li * K + 8 * g) * 2;
 #pragma unroll
-    for (int s = 0; s < G1::KS; ++s) xf[s] = ok ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < G1::KS; ++s) xf[s] = hvk_bld16(rx, o + 64 * s);
   };
   uint4 xf[G1::KS];
   load_x(tile, xf);
+  // the first tile's operands land before the loop: otherwise the loop header's wait serves
+  // both entries and becomes vmcnt(0) on every iteration (draining the stores in flight)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < G1::KS; ++s) hvk_launder(xf[s]);
   for (; tile < tiles; tile += stride) {
     asm volatile("" ::: "memory");
     uint4 xn[G1::KS];
     load_x(tile + stride, xn);
+    __builtin_amdgcn_sched_barrier(0);  // the next tile's loads issue here, not after the MFMAs
+    const auto rh = hvk_tile_rsrc(H, 16 * tile, M, N1 * 2), rg2 = hvk_tile_rsrc(Gh, 16 * tile, M, N1 * 2);
+    const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N2 * 2);
+    const uint32_t ho = (uint32_t)(li * N1 + 8 * g) * 2, yo = (uint32_t)(li * N2 + 8 * g) * 2;
     hvk_f32x4 acc[G1::NT];
 #pragma unroll
     for (int t = 0; t < G1::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
@@ -278,8 +298,6 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
     for (int s = 0; s < G1::KS; ++s)
 #pragma unroll
       for (int t = 0; t < G1::NT; ++t) acc[t] = hvk_mfma16(w1l[(t * G1::U4 + 4 * s + g) * 16 + li], xf[s], acc[t]);
-    const int row = 16 * tile + li;
-    const bool ok = row < M;
     hvk_f32x4 acc2[G2::NT];
 #pragma unroll
     for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_f32x4{0, 0, 0, 0};
@@ -293,33 +311,26 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
       }
       const uint4 hv = hvk_pack8(v);
       const uint4 gv = hvk_gelu8_bf16(hv);  // GELU of the rounded pre-activation, as the reference
-      if (ok) {
-        const size_t o = (size_t)row * N1 + 32 * j + 8 * g;
-        if (HVK_NT_SAVED & 1)
-          hvk_st16_nt(H + o, hv);
-        else
-          hvk_st16(H + o, hv);
-        hvk_st16(Gh + o, gv);
-      }
+      if (HVK_NT_SAVED & 1)
+        hvk_bst16_nt(rh, ho + 64 * j, hv);
+      else
+        hvk_bst16(rh, ho + 64 * j, hv);
+      hvk_bst16(rg2, ho + 64 * j, gv);
       // fc2 k-chunk j: this lane's GELU(h) of hidden units 32j + 8g .. +7 is the B fragment
 #pragma unroll
       for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
     }
-    if (ok) {
 #pragma unroll
-      for (int j = 0; j < G2::NT / 2; ++j) {
-        float v[8];
+    for (int j = 0; j < G2::NT / 2; ++j) {
+      float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc2[2 * j][r];
-          v[4 + r] = acc2[2 * j + 1][r];
-        }
-        if (b2) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += b2l[32 * j + 8 * g + e];
-        }
-        hvk_st16(Y + (size_t)row * N2 + 32 * j + 8 * g, hvk_pack8(v));
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc2[2 * j][r];
+        v[4 + r] = acc2[2 * j + 1][r];
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += b2l[32 * j + 8 * g + e];  // 0 without a bias
+      hvk_bst16(ry, yo + 64 * j, hvk_pack8(v));
     }
 #pragma unroll
     for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
@@ -359,34 +370,39 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __r
   }
   __syncthreads();
 
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  // branch-free global accesses through 16-row tile buffer views (see linear_kernel)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
   const int tiles = (M + 15) >> 4;
   const int stride = row_groups * WAVES;
   int tile = blockIdx.x * WAVES + wave;
   auto load_x = [&](int t, uint4 (&xf)[G1::KS]) {
-    const int row = 16 * t + li;
-    const bool ok = t < tiles && row < M;
-    const hvk_bf16* xp = GY + (size_t)row * K + 8 * g;
+    const auto rx = hvk_tile_rsrc(GY, 16 * t, M, K * 2);
+    const uint32_t o = (uint32_t)(li * K + 8 * g) * 2;
 #pragma unroll
-    for (int s = 0; s < G1::KS; ++s) xf[s] = ok ? hvk_ld16(xp + 32 * s) : make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < G1::KS; ++s) xf[s] = hvk_bld16(rx, o + 64 * s);
   };
   auto load_h = [&](int t, uint4 (&hf)[G1::NT / 2]) {
-    const int row = 16 * t + li;
-    const bool ok = t < tiles && row < M;
+    const auto rh = hvk_tile_rsrc(Hs, 16 * t, M, N1 * 2);
+    const uint32_t o = (uint32_t)(li * N1 + 8 * g) * 2;
 #pragma unroll
-    for (int j = 0; j < G1::NT / 2; ++j)
-      hf[j] = ok ? hvk_ld16(Hs + (size_t)row * N1 + 32 * j + 8 * g) : make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < G1::NT / 2; ++j) hf[j] = hvk_bld16(rh, o + 64 * j);
   };
   uint4 xf[G1::KS], hf[G1::NT / 2];
   load_x(tile, xf);
   load_h(tile, hf);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // see mlp_fwd_kernel
+#pragma unroll
+  for (int s = 0; s < G1::KS; ++s) hvk_launder(xf[s]);
+#pragma unroll
+  for (int j = 0; j < G1::NT / 2; ++j) hvk_launder(hf[j]);
   for (; tile < tiles; tile += stride) {
     asm volatile("" ::: "memory");
     uint4 xn[G1::KS], hn[G1::NT / 2];
     load_x(tile + stride, xn);
     load_h(tile + stride, hn);
-    const int row = 16 * tile + li;
-    const bool ok = row < M;
+    __builtin_amdgcn_sched_barrier(0);
+    const auto rgh = hvk_tile_rsrc(GH, 16 * tile, M, N1 * 2), rgx = hvk_tile_rsrc(GX, 16 * tile, M, N2 * 2);
+    const uint32_t ho = (uint32_t)(li * N1 + 8 * g) * 2, xo = (uint32_t)(li * N2 + 8 * g) * 2;
     hvk_f32x4 acc2[G2::NT];
 #pragma unroll
     for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_f32x4{0, 0, 0, 0};
@@ -418,22 +434,20 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __r
           v[e + 1] *= d.y;
         }
         const uint4 gv = hvk_pack8(v);
-        if (ok) hvk_st16(GH + (size_t)row * N1 + 32 * j + 8 * g, gv);
+        hvk_bst16(rgh, ho + 64 * j, gv);
 #pragma unroll
         for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
       }
     }
-    if (ok) {
 #pragma unroll
-      for (int j = 0; j < G2::NT / 2; ++j) {
-        float v[8];
+    for (int j = 0; j < G2::NT / 2; ++j) {
+      float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc2[2 * j][r];
-          v[4 + r] = acc2[2 * j + 1][r];
-        }
-        hvk_st16(GX + (size_t)row * N2 + 32 * j + 8 * g, hvk_pack8(v));
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc2[2 * j][r];
+        v[4 + r] = acc2[2 * j + 1][r];
       }
+      hvk_bst16(rgx, xo + 64 * j, hvk_pack8(v));
     }
 #pragma unroll
     for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];

@@ -156,6 +156,27 @@ __device__ __forceinline__ uint4 hvk_bld16(__amdgpu_buffer_rsrc_t r, uint32_t of
 __device__ __forceinline__ void hvk_bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hvk_u32x4, v), r, off, 0, 0);
 }
+__device__ __forceinline__ void hvk_bst16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hvk_u32x4, v), r, off, 0, 2);  // nt
+}
+__device__ __forceinline__ uint4 hvk_bld16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+}
+// pin a value as "defined here" (after an explicit s_waitcnt): the compiler then tracks no
+// pending memory operation on its registers
+__device__ __forceinline__ void hvk_launder(uint4& v) {
+  hvk_u32x4 t = __builtin_bit_cast(hvk_u32x4, v);
+  asm volatile("" : "+v"(t));
+  v = __builtin_bit_cast(uint4, t);
+}
+// Buffer view of the 16-row tile [r0, r0 + 16) of a row-major tensor (row_bytes per row),
+// clipped at M rows: rows past M read 0 and drop their stores, with no exec branch around the
+// accesses (r0 and base wave-uniform).  Offsets are lane-relative to row r0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hvk_tile_rsrc(const void* base, int r0, int M, int row_bytes) {
+  int rows = M - r0;
+  rows = rows < 0 ? 0 : (rows > 16 ? 16 : rows);
+  return hvk_rsrc(static_cast<const char*>(base) + (size_t)(r0 < M ? r0 : 0) * row_bytes, (size_t)rows * row_bytes);
+}
 __device__ __forceinline__ void hvk_st8(void* p, uint2 v) {
 #ifndef HVK_NT
   *reinterpret_cast<uint2*>(p) = v;
