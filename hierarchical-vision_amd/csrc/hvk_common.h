@@ -1,5 +1,6 @@
 // Shared device helpers for libhvk (gfx950 / CDNA4 only).
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <stdint.h>
@@ -334,6 +335,18 @@ __device__ __forceinline__ int hvk_pair_col(int gq) { return 16 * (gq & 1) + 8 *
 
 __device__ __forceinline__ float hvk_group4_sum(float v) { return hvk_xor32_sum(hvk_xor16_sum(v)); }
 __device__ __forceinline__ float hvk_group4_max(float v) { return hvk_xor32_max(hvk_xor16_max(v)); }
+
+// max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors)
+__device__ __forceinline__ float hvk_row16_max(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+  };
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>{}));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>{}));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>{}));  // row_mirror
+  return v;
+}
 
 __device__ __forceinline__ float hvk_wave_sum(float v) {
 #pragma unroll

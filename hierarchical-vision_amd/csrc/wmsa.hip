@@ -25,6 +25,7 @@
 // workgroup into an LDS table laid out in accumulator order; the shift mask is
 // recomputed from region bits only on edge windows.
 #include <stdlib.h>
+#include <string.h>
 
 #include "wmsa_common.h"
 
@@ -1181,7 +1182,13 @@ int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table
     const char* e = getenv("HVK_WMSA_FWD_V1");
     return e && atoi(e) > 0;
   }();
-  if (!v1 || lse) return hvk_wmsa::ring_fwd(a, B, H, W, C, num_heads, window, shift, st);
+  if (!v1 || lse) {
+    // HVK_WMSA_FWD_FORM=ring: the persistent slab-ring forward (A/B runs and parity tests; read
+    // per call); default: one workgroup per (window, head group)
+    const char* form = getenv("HVK_WMSA_FWD_FORM");
+    if (form && !strcmp(form, "ring")) return hvk_wmsa::ring_fwd(a, B, H, W, C, num_heads, window, shift, st);
+    return hvk_wmsa::win_fwd(a, B, H, W, C, num_heads, window, shift, st);
+  }
   int rc = make_geom(B, H, W, C, num_heads, window, shift, 256 * 4, a.g);
   if (rc) return rc;
   switch (window) {

@@ -38,12 +38,15 @@ __device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh
 }
 
 // L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
+// The squared norm comes from four v_dot2_f32_bf16 on the packed pairs (f32 accumulation).
 __device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post = 1.f) {
+  typedef __bf16 hvk_bf16x2 __attribute__((ext_vector_type(2)));
+  auto d2 = [](uint32_t w, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(hvk_bf16x2, w), __builtin_bit_cast(hvk_bf16x2, w), c, false);
+  };
+  float ss = d2(v.w, d2(v.z, d2(v.y, d2(v.x, 0.f))));
   float f[8];
   hvk_unpack8(v, f);
-  float ss = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
   ss = hvk_group4_sum(ss);
   // F.normalize: x / max(||x||, eps) == x * rsqrt(max(||x||^2, eps^2))
   rnorm = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
@@ -119,6 +122,21 @@ __device__ __forceinline__ uint4 lds16(const char* img, int off) {
   return *reinterpret_cast<const uint4*>(img + off);
 }
 
+// n / d for 0 <= n < 2^31 by a multiply-high (d >= 1 fixed at launch; host-side init):
+// s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1, q = (mulhi(n, m) + n) >> s
+struct FastDiv {
+  uint32_t m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return (uint32_t)(((uint64_t)__umulhi(n, f.m) + n) >> f.s);
+}
+
 struct FwdArgs {
   const hvk_bf16* qkv;       // [T, 3C]  x Wqkv^T + (q_bias, 0, 0)
   hvk_bf16* out;             // [T, C]
@@ -127,6 +145,7 @@ struct FwdArgs {
   float* lse;                // [T, nH] or null: per query, log2 of the softmax denominator of the
                              // log2e-scaled logits (the large-window backward's row constant)
   WmsaGeom g;
+  FastDiv fd_groups, fd_img, fd_ww;  // wmsa_win.hip: / (nH / HG), / (nWh nWw), / nWw
 };
 
 struct BwdArgs {
@@ -178,6 +197,9 @@ int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, floa
 // windows <= 8, forward (wmsa_ring.hip): one persistent workgroup per (window chunk, head
 // group), window slabs staged by LDS-DMA
 int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);
+// windows <= 8, forward (wmsa_win.hip): one workgroup per (window, head group), one LDS-DMA
+// burst per window, output rows stored from LDS
+int win_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);
 
 // finalize helper: per head block, write dscale / dq_bias from the workspace and zero it
 __device__ __forceinline__ void finalize_scale_qb(float* dscale_acc, float* dqb_acc, float* dscale,

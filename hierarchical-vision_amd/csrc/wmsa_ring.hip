@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
     for (int i = lane; i < K::R * K::R; i += 64) mb = fmaxf(mb, tb[i]);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) mb = fmaxf(mb, __shfl_xor(mb, m));
-    Mh = a.scale[h] * HVK_LOG2E + mb;
+    Mh = __builtin_fmaf(a.scale[h], HVK_LOG2E, mb);  // one rounding (wmsa_win.hip matches it)
     for (int i = lane; i < K::R * K::R; i += 64) tb[i] -= Mh;
   }
   const float sc2 = a.scale[h] * HVK_LOG2E;

@@ -32,9 +32,20 @@ def _inputs(B, H, W, nh, win, seed, std=1.0):
     return qkv, tab, scale
 
 
+def _force_form(monkeypatch, form):
+    """Windows <= 8: pick the forward form (wmsa_win.hip / wmsa_ring.hip) whatever the grid size
+    (by default grids of few resident rounds take the ring form)."""
+    monkeypatch.setenv("HVK_WMSA_FWD_FORM", form)
+    monkeypatch.setenv("HVK_WMSA_WIN_MIN_ROUNDS", "0")
+
+
+@pytest.mark.parametrize("form", ["win", "ring"])
 @pytest.mark.parametrize("B,H,W,nh,win,shift", CASES)
-def test_wmsa_forward_matches_oracle(B, H, W, nh, win, shift):
+def test_wmsa_forward_matches_oracle(monkeypatch, B, H, W, nh, win, shift, form):
     import hvamd.ops as ops
+    if win > 8 and form == "ring":
+        pytest.skip("one large-window form")
+    _force_form(monkeypatch, form)
     qkv, tab, scale = _inputs(B, H, W, nh, win, 1)
     ref = swinv2_ref.wmsa_core_ref(qkv, tab, scale, H, W, nh, win, shift)
     out = ops.window_attention_core(qkv.cuda().bfloat16(), tab.cuda(), scale.cuda(), H, W, nh,
@@ -117,15 +128,19 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
+@pytest.mark.parametrize("form", ["win", "ring"])
 @pytest.mark.parametrize("shared", [True, False])
 @pytest.mark.parametrize("B,H,W,nh,win,shift", LARGE_SCALE_CASES)
-def test_wmsa_scale100_anti_aligned_matches_oracle(B, H, W, nh, win, shift, shared):
+def test_wmsa_scale100_anti_aligned_matches_oracle(monkeypatch, B, H, W, nh, win, shift, shared, form):
     """The forward keeps the reference's softmax where the head-bound shift alone underflows:
     finite outputs and gradients, within max(1e-2 (2e-2 for gradients), 1.5x the reference's
     own bf16-autocast error) of the f32 oracle.  At scale 100 a bf16 rounding of q^ or k^
     (2^-9) moves a logit by ~0.04 nats, so the reference's AMP path itself is percent-level off
     its f32 path here; the bound follows it instead of pretending bf16 is f32."""
     import hvamd.ops as ops
+    if win > 8 and form == "ring":
+        pytest.skip("one large-window form")
+    _force_form(monkeypatch, form)
     qkv, tab, scale = _anti_aligned(B, H, W, nh, win, 11, shared)
     C = 32 * nh
     gout = torch.from_numpy(np.random.default_rng(5).standard_normal((B, H * W, C)).astype(np.float32))
@@ -156,6 +171,46 @@ def test_wmsa_scale100_anti_aligned_matches_oracle(B, H, W, nh, win, shift, shar
         errs[name] = (_rel(m, r), max(base, 1.5 * _rel(ra, r)))
     bad = {k: v for k, v in errs.items() if v[0] >= v[1]}
     assert not bad, (bad, errs)
+
+
+SMALL_CASES = [c for c in CASES if c[4] <= 8]
+
+
+@pytest.mark.parametrize("inputs", ["random", "anti100"])
+@pytest.mark.parametrize("B,H,W,nh,win,shift", SMALL_CASES)
+def test_wmsa_forward_forms_bit_identical(monkeypatch, B, H, W, nh, win, shift, inputs):
+    """Windows <= 8 have two forward forms with the same math: one workgroup per (window, head
+    group) (the default, wmsa_win.hip) and the persistent slab ring (HVK_WMSA_FWD_FORM=ring,
+    wmsa_ring.hip).  Outputs and the optional per-query row constants (lse) agree bit for bit,
+    on random inputs and on the scale-100 anti-aligned ones that take the row-max slow path;
+    the oracle comparisons above run the default form."""
+    import hvamd._lib as lib
+    from hvamd.ops import call, ptr, stream
+    if inputs == "random":
+        qkv, tab, scale = _inputs(B, H, W, nh, win, 7)
+    else:
+        qkv, tab, scale = _anti_aligned(B, H, W, nh, win, 8, shared=(B % 2 == 0))
+    lib.load()
+    C = 32 * nh
+    q = qkv.cuda().bfloat16().contiguous()
+    t, s = tab.cuda().contiguous(), scale.cuda().contiguous()
+    res = {}
+    for form in ("win", "ring"):
+        _force_form(monkeypatch, form)
+        for keep in (False, True):
+            out = torch.full((B, H * W, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+            lse = torch.full((B, H * W, nh), float("nan"), device="cuda") if keep else None
+            call("hvk_wmsa_fwd", ptr(q), ptr(out), ptr(lse), ptr(t), ptr(s), B, H, W, C, nh, win, shift,
+                 stream())
+            torch.cuda.synchronize()
+            res[form, keep] = (out.cpu(), None if lse is None else lse.cpu())
+    for keep in (False, True):
+        (ow, lw), (orr, lr) = res["win", keep], res["ring", keep]
+        assert torch.isfinite(ow.float()).all()
+        assert torch.equal(ow.view(torch.int16), orr.view(torch.int16)), (keep, (ow.float() - orr.float()).abs().max())
+        if keep:
+            assert torch.isfinite(lw).all() and torch.equal(lw, lr)
+    assert torch.equal(res["win", False][0].view(torch.int16), res["win", True][0].view(torch.int16))
 
 
 def test_wmsa_rejects_unsupported_head_dim():
