@@ -21,7 +21,7 @@
 #include "wmsa_ring.h"
 
 #ifndef HVK_WIN_PRIO  // 1: raised wave priority while a workgroup issues its DMA and its stores
-#define HVK_WIN_PRIO 1
+#define HVK_WIN_PRIO 0  // measured: neutral to -0.3 % (profiles/round3/wmsa_fwd_win/ab_prio.txt)
 #endif
 #ifndef HVK_WIN_PROBE  // tools/ probe builds: 1 memory only (no math), 2 math only (no DMA, no stores)
 #define HVK_WIN_PROBE 0

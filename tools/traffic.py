@@ -14,8 +14,9 @@ import glob
 import json
 import sys
 
-KERNELS = {"wmsa_fwd": "wmsa_fwd_ring_kernel", "wmsa_bwd": "wmsa_bwd_pair_kernel",
-           "mlp_fwd": "mlp_fwd_kernel", "mlp_bwd": "mlp_bwd_kernel"}  # the last two: fused stage-0 MLP
+# the forward: wmsa_fwd_win_kernel at stages 0-2, the ring form at stage 3 (all 12 launches)
+KERNELS = {"wmsa_fwd": ("wmsa_fwd_win_kernel", "wmsa_fwd_ring_kernel"), "wmsa_bwd": ("wmsa_bwd_pair_kernel",),
+           "mlp_fwd": ("mlp_fwd_kernel",), "mlp_bwd": ("mlp_bwd_kernel",)}  # the last two: fused stage-0 MLP
 
 
 def per_kernel(d, counter):
@@ -24,8 +25,8 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            for key, pat in KERNELS.items():
-                if pat in r["Kernel_Name"]:
+            for key, pats in KERNELS.items():
+                if any(p in r["Kernel_Name"] for p in pats):
                     out[key].append(float(r["Counter_Value"]))
     return out
 
