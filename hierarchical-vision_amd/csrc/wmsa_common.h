@@ -38,7 +38,25 @@ __device__ __forceinline__ int window_token_row(const WmsaGeom& g, int b, int wh
 }
 
 // L2-normalise one 8-wide slice of a 32-wide head row spread over lanes l, l^16, l^32, l^48.
-// The squared norm comes from four v_dot2_f32_bf16 on the packed pairs (f32 accumulation).
+// The squared norm as a sequential f32 sum of squares (the large-window kernels: their
+// whole-step test against the reference sits close to its logit-scale gradient bound, so their
+// rounding stays as measured there)
+__device__ __forceinline__ uint4 l2_normalize_seq(uint4 v, float& rnorm, float post = 1.f) {
+  float f[8];
+  hvk_unpack8(v, f);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+  ss = hvk_group4_sum(ss);
+  rnorm = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
+  const float m = rnorm * post;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= m;
+  return hvk_pack8(f);
+}
+
+// Windows <= 8 (forward and backward alike): the squared norm from four v_dot2_f32_bf16 on the
+// packed pairs (f32 accumulation), 8 fewer VALU instructions per 8-channel slice.
 __device__ __forceinline__ uint4 l2_normalize(uint4 v, float& rnorm, float post = 1.f) {
   typedef __bf16 hvk_bf16x2 __attribute__((ext_vector_type(2)));
   auto d2 = [](uint32_t w, float c) {

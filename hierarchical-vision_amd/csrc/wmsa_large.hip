@@ -227,7 +227,7 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
     for (int blk = wave; blk < F::BLK; blk += F::WAVES) {  // k^ in place
       const int off = fm16(16 * blk + li, gq);
       float rn;
-      *reinterpret_cast<uint4*>(kimg + off) = l2_normalize(lds16(kimg, off), rn);
+      *reinterpret_cast<uint4*>(kimg + off) = l2_normalize_seq(lds16(kimg, off), rn);
     }
     // this window's queries (normalised, times scale log2e): the loads are complete
     uint4 qf[QT];
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
       hvk_u32x4 v = __builtin_bit_cast(hvk_u32x4, qn[j]);
       asm volatile("" : "+v"(v));  // a fresh value: no compiler wait on the loads below
       float rn;
-      qf[j] = l2_normalize(__builtin_bit_cast(uint4, v), rn, sc2);
+      qf[j] = l2_normalize_seq(__builtin_bit_cast(uint4, v), rn, sc2);
     }
     const int b = cb, wh = cwh, ww = cww;
     if (++cww == g.nWw) {
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       if (blk < F::BLK) {
         float rn;
         const int off = fm16(16 * blk + li, gq);
-        *reinterpret_cast<uint4*>(img0 + off) = l2_normalize(ra[j], rn, post);
+        *reinterpret_cast<uint4*>(img0 + off) = l2_normalize_seq(ra[j], rn, post);
         *reinterpret_cast<uint4*>(img1 + off) = rb[j];
       }
     }
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       const int qy = pos / WIN, qxp = pos - qy * WIN;
       const int tq = K::RR - 1 - ((qy + WIN - 1) * K::R + qxp + WIN - 1);
       float rnq;
-      const uint4 qs = l2_normalize(cur.q, rnq, sc2);
+      const uint4 qs = l2_normalize_seq(cur.q, rnq, sc2);
       float rowc, delta;  // row constant (rel. to M_h) and delta for dS
       // S' (masked) and dP of (chunk c, half t)
       auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d) {
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       const int tk = K::RR - 1 + ky * K::R + kxp;  // mirrored entry of query bq: tk - bq
       const int bk = ky * K::R + kxp;
       float rnk;
-      const uint4 kh = l2_normalize(kc.k, rnk);
+      const uint4 kh = l2_normalize_seq(kc.k, rnk);
       hvk_f32x4 dk[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, dv[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
       auto loop2 = [&](auto edge_t) {
         constexpr bool EDGE = decltype(edge_t)::value;
