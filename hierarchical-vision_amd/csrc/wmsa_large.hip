@@ -471,6 +471,10 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
 // phase 2's q / dO rows, phase 2 the next window's k / v rows) and written to LDS between the
 // phases; every tile's own global inputs are loaded one tile ahead.  Interior windows and
 // unshifted blocks run mask-free copies of both loops.
+#ifndef HVK_LARGE_PROBE  // tools/ timing probes of the backward's phase 2 (results wrong)
+#define HVK_LARGE_PROBE 0
+#endif
+
 template <int WIN>
 struct BCfg {
   using K = LCfg<WIN>;
@@ -895,8 +899,12 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
             const hvk_f32x4 c4 = {tp[0], tp[-1], tp[-2], tp[-3]};
             hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), kh, c4);
             const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), kc.v, hvk_f32x4{0, 0, 0, 0});
+#if HVK_LARGE_PROBE == 2  // probe: row constants not read (wrong values, timing only)
+            const float4 l4 = make_float4(rnk, rnk, rnk, rnk), d4 = l4;
+#else
             const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
             const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);
+#endif
             const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
             if (EDGE) {
               const bool rmis = edge_r && ((ky >= lim) != (qyy[t] >= lim));
@@ -919,6 +927,9 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
           // bin across the lanes (strided key tiles); the compiler fences keep one batch's reads
           // behind the previous batch's writes.  (LDS float atomics instead -- ds_add_f32, one op
           // per element -- ran the w24 backward 4.9x slower: profiles/round3/large_bins_atomic_ab.txt)
+#if HVK_LARGE_PROBE == 1  // probe: no CPB-gradient bins (wrong values, timing only)
+          if (false)
+#endif
 #pragma unroll
           for (int b0 = 0; b0 < 8; b0 += F::BATCH) {
             float v[F::BATCH];

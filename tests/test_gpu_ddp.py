@@ -93,7 +93,8 @@ def test_rccl_one_rank_buckets_match_plain_step():
     forced on runs the hook-launched all-reduces on RCCL's stream, synchronize() and the
     fused step on the bucket views; with one rank the exchange is the identity, so two steps
     must equal two steps without buckets up to the run-to-run order of the backward's
-    bias-table atomics (1e-4 relative per tensor; a lost, doubled or stale gradient is O(1))."""
+    bias-table atomics (1e-3 relative per tensor: measured up to 1.9e-4 between runs; a lost,
+    doubled or stale gradient is O(1))."""
     from hvamd import hierarchy, models, optim, swinv2
     from hvamd.algorithmic import GradientClipping
     from hvamd.ddp import GradientBuckets
@@ -131,4 +132,4 @@ def test_rccl_one_rank_buckets_match_plain_step():
     b = run(False)
     for u, v in zip(a, b):
         rel = ((u - v).norm() / v.norm().clamp_min(1e-12)).item()
-        assert rel < 1e-4, rel
+        assert rel < 1e-3, rel
