@@ -164,6 +164,7 @@ struct FwdArgs {
                              // log2e-scaled logits (the large-window backward's row constant)
   WmsaGeom g;
   FastDiv fd_groups, fd_img, fd_ww;  // wmsa_win.hip: / (nH / HG), / (nWh nWw), / nWw
+  int dma_nt;                         // wmsa_win.hip: slab DMA with the nontemporal hint
 };
 
 struct BwdArgs {

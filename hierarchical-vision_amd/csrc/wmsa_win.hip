@@ -23,6 +23,9 @@
 #ifndef HVK_WIN_PRIO  // 1: raised wave priority while a workgroup issues its DMA and its stores
 #define HVK_WIN_PRIO 0  // measured: neutral to -0.3 % (profiles/round3/wmsa_fwd_win/ab_prio.txt)
 #endif
+#ifndef HVK_WIN_REGSTORE  // A/B builds: 1 stores each head's output slice from registers (no LDS staging)
+#define HVK_WIN_REGSTORE 0
+#endif
 #ifndef HVK_WIN_PROBE  // tools/ probe builds: 1 memory only (no math), 2 math only (no DMA, no stores)
 #define HVK_WIN_PROBE 0
 #endif
@@ -116,7 +119,10 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
         asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + j * 1024) + 16u * lane),
                      "v"(hvk_u32x4{0, 0, 0, 0}) : "memory");
 #else
-        __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 2);
+        if (a.dma_nt)
+          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 2);
+        else
+          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 0);
 #endif
       }
     }
@@ -371,7 +377,11 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       const float inv = __builtin_amdgcn_rcpf(osum[0]);
       const uint4 v = make_uint4(hvk_pack2(o[0][0] * inv, o[0][1] * inv), hvk_pack2(o[0][2] * inv, o[0][3] * inv),
                                  hvk_pack2(o[1][0] * inv, o[1][1] * inv), hvk_pack2(o[1][2] * inv, o[1][3] * inv));
+#if HVK_WIN_REGSTORE
+      *reinterpret_cast<uint4*>(a.out + (size_t)window_token_row(g, b, wh, ww, WIN, tq) * C + h * 32 + 8 * gq) = v;
+#else
       lds_wr128(fb + (16 / K::PW) * qi * K::RUN * 16, v);
+#endif
       if constexpr (LSE) {
         if (gq == 0)
           a.lse[(size_t)window_token_row(g, b, wh, ww, WIN, tq) * g.nH + h] = Mh + lshift + __log2f(osum[0]);
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   }
 
 #endif  // HVK_WIN_PROBE != 1
-#if HVK_WIN_PROBE == 2
+#if HVK_WIN_PROBE == 2 || HVK_WIN_REGSTORE
   return;
 #endif
   // 6. the window's output row segments, HG*64 contiguous bytes per token, from the q slots
@@ -435,6 +445,14 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
   a.fd_groups = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nH / HG));
   a.fd_img = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nWh * a.g.nWw));
   a.fd_ww = hvk_wmsa::make_fastdiv((uint32_t)a.g.nWw);
+  // slab DMA cache policy (HVK_WMSA_WIN_NT, A/B runs): 2 (default) nontemporal only when qkv
+  // exceeds the 256 MB Infinity Cache -- the qkv GEMM just wrote it, so a smaller one is read
+  // from the cache (SwinV2-T stages 1-3; stage 0's 462 MB streams nontemporally): in-step
+  // 0.630-0.632 of 8 TB/s vs 0.610 always nontemporal vs 0.570 never (one box,
+  // profiles/round3/wmsa_fwd_win/ab_dma_policy.txt); 1 always, 0 never
+  const char* nt = getenv("HVK_WMSA_WIN_NT");
+  const int ntm = nt ? atoi(nt) : 2;
+  a.dma_nt = ntm == 2 ? ((long long)a.g.B * a.g.H * a.g.W * a.g.C * 6 > (256ll << 20)) : ntm != 0;
   const long long grid = (items + 7) / 8 * 8;
   if (grid > 0x7fffffffLL) return hvk_set_error(HVK_EINVAL, "wmsa win: %lld windows x groups", items);
   HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_win_kernel<WIN, HG, LSE>), dim3((unsigned)grid), dim3(64 * HG),
