@@ -1177,6 +1177,9 @@ int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table
   }
   if (window != 4 && window != 6 && window != 7 && window != 8)
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: window %d not built (4,6,7,8,12,16,24)", window);
+  // the w <= 8 forms address one image's qkv rows with 32-bit byte offsets, token rows as int
+  if ((long long)H * W * C * 6 >= (1ll << 32) || (long long)B * H * W >= (1ll << 31))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd: %d x %d x %d x %d past 32-bit offsets", B, H, W, C);
   // HVK_WMSA_FWD_V1=1: the round-1 wave-per-(window, head) kernel (A/B timing only)
   static const bool v1 = [] {
     const char* e = getenv("HVK_WMSA_FWD_V1");

@@ -418,7 +418,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       y -= y >= g.H ? g.H : 0;
       x -= x >= g.W ? g.W : 0;
       const int row = (int)HVK_BCHECK(__umul24((uint32_t)y, (uint32_t)g.W) + x, g.H * g.W);  // in image b
-      off[k] = __umul24((uint32_t)row, C2) + c * 16;  // < 2^31: launch_win_ checks H W C 2
+      off[k] = __umul24((uint32_t)row, C2) + c * 16;  // < 2^32: hvk_wmsa_fwd bounds H W 6C
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -440,8 +440,8 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
     attr = true;
   }
   const long long items = (long long)a.g.n_windows * (a.g.nH / HG);
-  if ((long long)a.g.H * a.g.W * a.g.C * 2 >= (1ll << 31) || a.g.H * a.g.W >= (1 << 24))
-    return hvk_set_error(HVK_EUNSUPPORTED, "wmsa win: %d x %d x %d image too large", a.g.H, a.g.W, a.g.C);
+  if (a.g.H * a.g.W >= (1 << 24))  // launch_win routes these to the ring form
+    return hvk_set_error(HVK_EINVAL, "wmsa win: %d x %d image past 24-bit token offsets", a.g.H, a.g.W);
   a.fd_groups = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nH / HG));
   a.fd_img = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nWh * a.g.nWw));
   a.fd_ww = hvk_wmsa::make_fastdiv((uint32_t)a.g.nWw);
@@ -470,7 +470,10 @@ int launch_win(FwdArgs& a, hipStream_t st) {
   const double min_rounds = mr ? atof(mr) : 2.5;
   const int per_cu = (160 * 1024) / RingCfg<WIN, HG>::LDS;
   const double rounds = (double)a.g.n_windows * (a.g.nH / HG) / (256.0 * (per_cu > 0 ? per_cu : 1));
-  if (rounds < min_rounds)
+  // per-image byte offsets of the output stores are 32-bit (24-bit multiplies): larger images
+  // take the ring form, which addresses with 64-bit offsets
+  const bool big = a.g.H * a.g.W >= (1 << 24);  // (hvk_wmsa_fwd bounds H W 6C below 2^32)
+  if (rounds < min_rounds || big)
     return hvk_wmsa::ring_fwd(a, a.g.B, a.g.H, a.g.W, a.g.C, a.g.nH, WIN, a.g.shift, st);
   return a.lse ? launch_win_<WIN, HG, true>(a, st) : launch_win_<WIN, HG, false>(a, st);
 }

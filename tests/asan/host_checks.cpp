@@ -34,6 +34,8 @@ int main() {
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 10, 10, 96, 3, 5, 0, nullptr) == HVK_EUNSUPPORTED);
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 15, 15, 96, 3, 7, 3, nullptr) == HVK_EINVAL);
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 14, 14, 96, 3, 7, 7, nullptr) == HVK_EINVAL);
+  // w <= 8: one image's qkv past 32-bit byte offsets (7168^2 tokens x 6C) -> refused, no launch
+  EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 7168, 7168, 96, 3, 7, 3, nullptr) == HVK_EUNSUPPORTED);
   for (int w : {4, 6, 7, 8, 12, 16, 24})
     for (int nh = 1; nh <= 32; ++nh) {
       const size_t ws = hvk_wmsa_bwd_workspace_bytes(nh, w);
