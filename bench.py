@@ -143,6 +143,34 @@ def wmsa_work(model, batch):
     return w
 
 
+def stage_breakdown(model, batch, durations_ms, per_elem, backward):
+    """Per-stage view of the timed W-MSA launches (libhvk's per-launch dispatch-packet times,
+    in launch order): a step launches one per SwinTransformerBlock, forward in block order and
+    backward in reverse, so launch i belongs to block i mod (blocks); grouped by the block's
+    resolution: mean duration, algorithmic bytes (per_elem * T * C) and rate against 8 TB/s."""
+    from hvamd.swinv2 import SwinTransformerBlock
+    blocks = [m for m in model.modules() if isinstance(m, SwinTransformerBlock)]
+    if not blocks or not durations_ms or len(durations_ms) % len(blocks):
+        return None
+    order = blocks[::-1] if backward else blocks
+    groups = {}
+    for i, ms in enumerate(durations_ms):
+        m = order[i % len(blocks)]
+        key = (tuple(m.input_resolution), m.dim, m.window_size)
+        g = groups.setdefault(key, [0.0, 0, per_elem * batch * m.input_resolution[0] * m.input_resolution[1] * m.dim])
+        g[0] += ms
+        g[1] += 1
+    out = []
+    for (res, dim, win), (ms, n, nbytes) in sorted(groups.items(), key=lambda kv: -kv[0][0][0]):
+        avg = ms / n
+        gbs = nbytes / (avg / 1000) / 1e9
+        out.append({"resolution": list(res), "dim": dim, "window": win,
+                    "launches_per_step": n * len(blocks) // len(durations_ms),
+                    "avg_launch_us": round(1000 * avg, 2), "bytes_per_launch": nbytes,
+                    "achieved_gbs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)})
+    return out
+
+
 def kernel_names(windows):
     # w <= 8: one workgroup per (window, head group) (wmsa_win.hip); grids of under 2.5 resident
     # rounds (SwinV2-T stage 3) take the persistent ring form (wmsa_ring.hip)
@@ -281,7 +309,7 @@ def main():
 
     work = wmsa_work(model.module, args.batch)
     timing = not args.no_roofline
-    timer, timed_steps = None, args.steps
+    timer, timed_steps, launches = None, args.steps, None
     if args.graph:
         # eager warm-up; the last roofline_steps of it carry the W-MSA kernel timer (graph
         # replays cannot: per-kernel dispatch events are not captured), then capture
@@ -293,6 +321,7 @@ def main():
             trainer.train_step(batch)
         if timing:
             torch.cuda.synchronize()
+            launches = {k: ops.kernel_timer_launches(k) for k in (0, 1)}
             timer, timed_steps = ops.kernel_timer_stop(), rsteps
         trainer.capture(batch)
         step = trainer.replay
@@ -319,6 +348,7 @@ def main():
     elapsed = time.perf_counter() - t0
     gemm_timer, gemm_steps = None, 0
     if timing and not args.graph:
+        launches = {k: ops.kernel_timer_launches(k) for k in (0, 1)}
         timer = ops.kernel_timer_stop()
         gemm_steps = min(args.steps, 5)
         ops.kernel_timer_start(kinds=ops.TIMER_GEMM)
@@ -382,10 +412,14 @@ def main():
         if traffic is not None:
             r["algorithmic_bytes_per_launch"] = work["fwd_bytes"] // n_launch
             r["traffic_source"] = TRAFFIC_SOURCE
+        if launches:
+            r["stages"] = stage_breakdown(model.module, args.batch, launches[0], 8, False)
         result["roofline"] = r
         result["roofline_bwd"] = roofline_block(
             kb, work["bwd_bytes"], work["bwd_flops"], bw_ms, bw_n, timed_steps,
             measured_traffic("wmsa_bwd") if default_cfg else None, work["bwd_exp"] if large else None)
+        if launches:
+            result["roofline_bwd"]["stages"] = stage_breakdown(model.module, args.batch, launches[1], 16, True)
         # dense contractions on libhvk's MFMA GEMMs (every Linear but the classifier head):
         # their algorithmic flops (2 M N K per launch, summed by the library) over their
         # dispatch-packet-timed durations

@@ -25,6 +25,7 @@ SIGNATURES = {
     "hvk_kernel_timer_read": (_i, [_i, _p, _p]),
     "hvk_kernel_timer_read_work": (_i, [_i, _p, _p, _p]),
     "hvk_kernel_timer_kinds": (_i, [_i]),
+    "hvk_kernel_timer_launch": (_i, [_i, _p, _p, _p]),
     "hvk_last_error_string": (ctypes.c_char_p, []),
     "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),

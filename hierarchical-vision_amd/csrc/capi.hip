@@ -84,6 +84,20 @@ int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double
   return HVK_OK;
 }
 
+int hvk_kernel_timer_launch(int index, int* kind, double* ms, double* work) {
+  if (!kind || !ms) return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_launch: null pointer");
+  if (index < 0 || (size_t)index >= g_timer_used)
+    return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_launch: index %d of %zu", index, g_timer_used);
+  const TimerRec& r = g_timer[index];
+  float t = 0.f;
+  if (hipEventSynchronize(r.stop) != hipSuccess || hipEventElapsedTime(&t, r.start, r.stop) != hipSuccess)
+    return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_launch: event query failed");
+  *kind = r.kind;
+  *ms = t;
+  if (work) *work = r.work;
+  return HVK_OK;
+}
+
 int hvk_kernel_timer_read(int kind, double* total_ms, int* launches) {
   return hvk_kernel_timer_read_work(kind, total_ms, launches, nullptr);
 }

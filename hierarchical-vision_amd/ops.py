@@ -24,6 +24,19 @@ def kernel_timer_start(max_launches=32768, kinds=TIMER_ALL):
     call("hvk_kernel_timer_enable", int(max_launches))
 
 
+def kernel_timer_launches(kind):
+    """Durations (ms) of the timed launches of one kind, in launch order (call before
+    kernel_timer_stop)."""
+    out, i = [], 0
+    k, t, w = ctypes.c_int(0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+    lib = _lib.load()
+    while lib.hvk_kernel_timer_launch(i, ctypes.byref(k), ctypes.byref(t), ctypes.byref(w)) == 0:
+        if k.value == kind:
+            out.append(t.value)
+        i += 1
+    return out
+
+
 def kernel_timer_stop():
     """Stop timing; returns {"wmsa_fwd" | "wmsa_bwd" | "gemm" | "wgrad": (total_ms, launches,
     summed algorithmic work)} (GEMM work = 2 M N K flops per launch)."""

@@ -44,6 +44,9 @@ int hvk_kernel_timer_read(int kind, double* total_ms, int* launches);
  * W-MSA launches inside its timed steps and the GEMMs in extra steps after them */
 int hvk_kernel_timer_kinds(int mask);
 int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double* work);
+/* the index-th timed launch since hvk_kernel_timer_enable, in launch order: its kind, duration
+ * and the work the library recorded for it (bench.py's per-stage W-MSA breakdown) */
+int hvk_kernel_timer_launch(int index, int* kind, double* ms, double* work);
 
 /* ---- Shifted-window cosine attention core ------------------------------------------
  * Replaces swinv2.py:399-412 (roll + window_partition), 221-261 (WindowAttention core:

@@ -49,3 +49,24 @@ def test_roofline_block_picks_the_binding_roof(ai, bound):
         assert r["unit"] == "TFLOP/s" and r["frac"] == r["mfma_frac"]
     assert r["avg_launch_us"] == pytest.approx(500.0)
     assert r["ms_per_step"] == pytest.approx(1.0)
+
+
+def test_stage_breakdown_groups_launches_by_block_resolution():
+    """bench.py's per-stage view: launch i of a step belongs to block i mod 12 (forward order;
+    the backward in reverse), grouped by resolution with the per-launch bytes of SURVEY.md §8(d)."""
+    import bench
+    from hvamd import swinv2
+    net = swinv2.SwinTransformerV2(img_size=224, embed_dim=96, depths=[2, 2, 6, 2],
+                                   num_heads=[3, 6, 12, 24], window_size=7, num_classes=10)
+    per_stage_us = [100.0, 50.0, 30.0, 20.0]
+    fwd = [per_stage_us[s] / 1000 for s in [0, 0, 1, 1, 2, 2, 2, 2, 2, 2, 3, 3]] * 3  # 3 steps
+    st = bench.stage_breakdown(net, 256, fwd, 8, backward=False)
+    assert [g["resolution"] for g in st] == [[56, 56], [28, 28], [14, 14], [7, 7]]
+    assert [g["launches_per_step"] for g in st] == [2, 2, 6, 2]
+    assert [g["avg_launch_us"] for g in st] == per_stage_us
+    assert st[0]["bytes_per_launch"] == 8 * 256 * 56 * 56 * 96
+    assert st[0]["achieved_gbs"] == pytest.approx(8 * 256 * 56 * 56 * 96 / 100e-6 / 1e9, rel=1e-3)
+    bwd = fwd[::-1]  # the backward launches stage 3 first
+    sb = bench.stage_breakdown(net, 256, bwd, 16, backward=True)
+    assert [g["avg_launch_us"] for g in sb] == per_stage_us
+    assert bench.stage_breakdown(net, 256, fwd[:5], 8, backward=False) is None
