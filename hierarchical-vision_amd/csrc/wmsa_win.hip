@@ -47,7 +47,10 @@ __device__ __forceinline__ void lds_wr128(uint32_t a, uint4 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(__builtin_bit_cast(hvk_u32x4, v)) : "memory");
 }
 
-template <int WIN, int HG, bool LSE>
+// MM: shift-mask form, fixed at launch so no branch (and no register copies where branches
+// merge) sits in the score loop: 0 unshifted block (no mask), 1 w7 / shift 3 (tile-uniform
+// row band + per-lane column band: one add per element, every window), 2 any other shift
+template <int WIN, int HG, bool LSE, int MM>
 __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   using K = RingCfg<WIN, HG>;
   constexpr int NE = (K::TABF + 63) / 64;  // bias-table entries per lane
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   // 5. attention, one query tile at a time (the ring kernel's math); the normalised output row
   //    slice goes back into this head's q slots of the slab (read above by this wave only)
   const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
-  const bool MASK7 = WIN == 7 && K::PW == 8 && g.shift == 3;
+  static_assert(MM != 1 || (WIN == 7 && K::PW == 8), "the tile-uniform mask form is w7 / shift 3 only");
   const float colmask = (edge_c && (((li >> 2) ^ gq) & 1)) ? mask2 : 0.f;  // query x >= 4 vs key x >= 4
   float rn;
 #pragma unroll
@@ -281,16 +284,17 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
         s[ki] = hvk_mfma16(kf[ki], qf[qi], bb);
       }
       settle_tiles(s);
-      if (MASK7 && (edge_r || edge_c)) {
+      if constexpr (MM == 1) {
         // w7, shift 3 on the 8-wide grid: the row band of a tile pair is uniform (bands = tiles
         // {0,1} / {2,3}) and the column band of a lane's keys is fixed by gq: one add per element
+        // on every window (0 on interior ones: s + 0 = s), no branch
 #pragma unroll
         for (int ki = 0; ki < K::NT; ++ki) {
           const float mv = (edge_r && ((qi >= 2) != (ki >= 2))) ? mask2 : colmask;
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[ki][r] += mv;
         }
-      } else if (edge_r || edge_c) {
+      } else if (MM == 2 && (edge_r || edge_c)) {
         const int qy = pq / K::PW, qx = pq % K::PW;
         uint32_t mreg = 0;
         if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
@@ -430,12 +434,12 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   }
 }
 
-template <int WIN, int HG, bool LSE>
+template <int WIN, int HG, bool LSE, int MM>
 int launch_win_(FwdArgs& a, hipStream_t st) {
   using K = RingCfg<WIN, HG>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_win_kernel<WIN, HG, LSE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_fwd_win_kernel<WIN, HG, LSE, MM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
     attr = true;
   }
@@ -455,7 +459,7 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
   a.dma_nt = ntm == 2 ? ((long long)a.g.B * a.g.H * a.g.W * a.g.C * 6 > (256ll << 20)) : ntm != 0;
   const long long grid = (items + 7) / 8 * 8;
   if (grid > 0x7fffffffLL) return hvk_set_error(HVK_EINVAL, "wmsa win: %lld windows x groups", items);
-  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_win_kernel<WIN, HG, LSE>), dim3((unsigned)grid), dim3(64 * HG),
+  HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_win_kernel<WIN, HG, LSE, MM>), dim3((unsigned)grid), dim3(64 * HG),
                    K::LDS, st, a);
   HVK_CHECK_LAUNCH("wmsa_fwd_win");
   return HVK_OK;
@@ -475,7 +479,10 @@ int launch_win(FwdArgs& a, hipStream_t st) {
   const bool big = a.g.H * a.g.W >= (1 << 24);  // (hvk_wmsa_fwd bounds H W 6C below 2^32)
   if (rounds < min_rounds || big)
     return hvk_wmsa::ring_fwd(a, a.g.B, a.g.H, a.g.W, a.g.C, a.g.nH, WIN, a.g.shift, st);
-  return a.lse ? launch_win_<WIN, HG, true>(a, st) : launch_win_<WIN, HG, false>(a, st);
+  if (a.g.shift == 0) return a.lse ? launch_win_<WIN, HG, true, 0>(a, st) : launch_win_<WIN, HG, false, 0>(a, st);
+  if constexpr (WIN == 7)
+    if (a.g.shift == 3) return a.lse ? launch_win_<WIN, HG, true, 1>(a, st) : launch_win_<WIN, HG, false, 1>(a, st);
+  return a.lse ? launch_win_<WIN, HG, true, 2>(a, st) : launch_win_<WIN, HG, false, 2>(a, st);
 }
 
 template <int WIN>
