@@ -18,6 +18,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "wmsa_ring.h"
 
 #ifndef HVK_WIN_PRIO  // 1: raised wave priority while a workgroup issues its DMA and its stores
@@ -42,6 +44,21 @@ __device__ __forceinline__ uint32_t gld32(const float* p) {
 }
 __device__ __forceinline__ void lds_wr32(uint32_t a, float v) {
   asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+// one LDS-DMA wave-instruction (global_load_lds_dwordx4) from inline asm: wave-uniform base
+// (scalar pair) + 32-bit lane offset, M0 = the LDS destination; invisible to the compiler's
+// waitcnt pass (the kernel counts vmcnt itself)
+template <bool NT>
+__device__ __forceinline__ void dma16_lds(const char* base, uint32_t voff, uint32_t m0) {
+  const uint64_t b = (uint64_t)base;
+  const uint64_t bs = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt"
+                 :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                 :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
 }
 __device__ __forceinline__ void lds_wr128(uint32_t a, uint4 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(__builtin_bit_cast(hvk_u32x4, v)) : "memory");
@@ -109,26 +126,38 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
     const char* img = reinterpret_cast<const char*>(a.qkv) + (size_t)b * g.H * WRB;
     const int y0 = wh * WIN + g.shift, x0 = ww * WIN + g.shift;
     const int ly = g.H - y0, lx = g.W - x0;  // ty >= ly (tx >= lx): the row wraps (cyclic shift)
+    // per-lane offsets with this window's column wrap applied, materialised once (4 VGPRs):
+    // an instruction then adds only its uniform row offset
 #pragma unroll
-    for (int k = 0; k < K::NK; ++k) {
-      const int j = wave + HG * k;
-      if (j < K::NINST) {
-        const int ty = j / K::IPR;
-        const unsigned U = ((unsigned)(y0 + ty - (ty >= ly ? g.H : 0)) * g.W + x0) * RB;  // uniform
-        unsigned off = __umul24(pre[k % K::KP], 1u) + U;  // v_mad_u32_u24: low 24 bits of pre
-        if (lx < WIN) off -= ((int)(pre[k % K::KP] >> 24) >= lx) ? WRB : 0u;
-#if HVK_WIN_PROBE == 2
-        (void)off;
-        asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + j * 1024) + 16u * lane),
-                     "v"(hvk_u32x4{0, 0, 0, 0}) : "memory");
-#else
-        if (a.dma_nt)
-          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 2);
-        else
-          __builtin_amdgcn_global_load_lds((gbl_vptr)(img + off), (lds_vptr)(smem + j * 1024), 16, 0, 0);
-#endif
-      }
+    for (int k = 0; k < K::KP; ++k) {
+      pre[k] = __umul24(pre[k], 1u) - ((lx < WIN && (int)(pre[k] >> 24) >= lx) ? WRB : 0u);
+      lds_fence(pre[k]);
     }
+    __builtin_assume(wave < HG);
+    // the DMA from inline asm (scalar base + 32-bit lane offset, M0 = the LDS destination):
+    // 1-2 VALU per instruction; the cache policy (nontemporal or not) picks one of two loops
+    auto issue = [&](auto nt_t) {
+#pragma unroll
+      for (int k = 0; k < K::NK; ++k) {
+        const int j = wave + HG * k;
+        if (j < K::NINST) {
+          const int ty = j / K::IPR;
+          const unsigned U = ((unsigned)(y0 + ty - (ty >= ly ? g.H : 0)) * g.W + x0) * RB;  // uniform
+          const unsigned off = pre[k % K::KP] + U;
+#if HVK_WIN_PROBE == 2
+          (void)off;
+          asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + j * 1024) + 16u * lane),
+                       "v"(hvk_u32x4{0, 0, 0, 0}) : "memory");
+#else
+          dma16_lds<decltype(nt_t)::value>(img, off, lds_addr(smem) + (uint32_t)j * 1024u);
+#endif
+        }
+      }
+    };
+    if (a.dma_nt)
+      issue(std::true_type{});
+    else
+      issue(std::false_type{});
   }
 
   if (HVK_WIN_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -265,6 +294,10 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
     qf[i] = l2_normalize(qf[i], rn, sc2);
     kf[i] = l2_normalize(kf[i], rn);
   }
+  // the query-tile loop is instantiated twice, for windows with and without a shift mask: the
+  // branch sits outside it, so nothing inside merges registers from two paths
+  auto run_tiles = [&](auto edge_t) {
+  constexpr bool EDGE = decltype(edge_t)::value;
 #pragma unroll
   for (int qi = 0; qi < K::NT; ++qi) {
     const int pq = 16 * qi + li;
@@ -284,17 +317,17 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
         s[ki] = hvk_mfma16(kf[ki], qf[qi], bb);
       }
       settle_tiles(s);
-      if constexpr (MM == 1) {
+      if constexpr (MM == 1 && EDGE) {
         // w7, shift 3 on the 8-wide grid: the row band of a tile pair is uniform (bands = tiles
         // {0,1} / {2,3}) and the column band of a lane's keys is fixed by gq: one add per element
-        // on every window (0 on interior ones: s + 0 = s), no branch
+        // (edge windows only)
 #pragma unroll
         for (int ki = 0; ki < K::NT; ++ki) {
           const float mv = (edge_r && ((qi >= 2) != (ki >= 2))) ? mask2 : colmask;
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[ki][r] += mv;
         }
-      } else if (MM == 2 && (edge_r || edge_c)) {
+      } else if constexpr (MM == 2 && EDGE) {
         const int qy = pq / K::PW, qx = pq % K::PW;
         uint32_t mreg = 0;
         if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
@@ -327,7 +360,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(tq >= 0 && !(osum[0] >= 0x1p-100f)) != 0, 0)) {
       // slow path (rare, wave-uniform): the reference's softmax with the true row max
       uint32_t mreg = 0;
-      if (edge_r || edge_c) {
+      if constexpr (EDGE) {
         const int qy = pq / K::PW, qx = pq % K::PW;
         if (edge_r) mreg |= (kband ^ (qy >= WIN - g.shift ? 0xFFFFu : 0u)) & 0xFFFFu;
         if (edge_c) mreg |= (kband >> 16) ^ (qx >= WIN - g.shift ? 0xFFFFu : 0u);
@@ -392,6 +425,11 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       }
     }
   }
+  };
+  if (MM != 0 && (edge_r || edge_c))
+    run_tiles(std::true_type{});
+  else
+    run_tiles(std::false_type{});
 
 #endif  // HVK_WIN_PROBE != 1
 #if HVK_WIN_PROBE == 2 || HVK_WIN_REGSTORE
