@@ -60,6 +60,13 @@ __device__ __forceinline__ void dma16_lds(const char* base, uint32_t voff, uint3
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
                  :: "s"(__builtin_amdgcn_readfirstlane(m0)), "v"(voff), "s"((const void*)bs) : "memory");
 }
+// a * b + c on the full-rate 24-bit multiplier (a, b < 2^24): from asm, so the compiler cannot
+// fold it into a quarter-rate v_mad_u64_u32 / v_mul_lo_u32
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ void lds_wr128(uint32_t a, uint4 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(__builtin_bit_cast(hvk_u32x4, v)) : "memory");
 }
@@ -118,9 +125,10 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
     for (int k = 0; k < K::KP; ++k) {
       const int m = (wave + HG * k) % K::IPR;
       const unsigned q = 64u * m + lane;
-      const unsigned tx = q / K::RS, r = q - tx * K::RS;
-      const unsigned part = r / (4 * HG), c = r - part * (4 * HG);
-      const unsigned v = (__umul24(tx, RB) + __umul24(part, 2u * C) + c * 16 + grp_off) | (tx << 24);
+      // slot q = RS tx + 4HG part + c with RS = 3 (4HG): u = q / 4HG = 3 tx + part, and the byte
+      // offset tx 6C + part 2C = u 2C
+      const unsigned u = q / (4 * HG), c = q - mad24(u, 4u * HG, 0u), tx = u / 3;
+      const unsigned v = (__umul24(u, 2u * C) + c * 16 + grp_off) | (tx << 24);
       pre[k] = q < (unsigned)(WIN * K::RS) ? v : (unsigned)grp_off;
     }
     const char* img = reinterpret_cast<const char*>(a.qkv) + (size_t)b * g.H * WRB;
@@ -230,7 +238,10 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       rowb |= ((16 / K::PW) * ki + (4 * gq) / K::PW >= lim) ? 0xFu << (4 * ki) : 0u;
     const int cl = lim - (4 * gq) % K::PW;  // column r in band iff r >= cl
     const uint32_t nib = cl <= 0 ? 0xFu : (cl >= 4 ? 0u : (0xFu << cl) & 0xFu);
-    kband = rowb | ((nib * (K::NT == 4 ? 0x1111u : K::NT == 3 ? 0x111u : K::NT == 2 ? 0x11u : 0x1u)) << 16);
+    uint32_t rep = nib;
+#pragma unroll
+    for (int ki = 1; ki < K::NT; ++ki) rep |= nib << (4 * ki);  // nibble per key tile, no multiply
+    kband = rowb | (rep << 16);
   }
 
   // 4. the slab has landed (every wave's DMA + table writes): fragments into registers
@@ -445,29 +456,35 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
     constexpr int NS = (K::N * SEG + 64 * HG - 1) / (64 * HG);
     static_assert(64 * HG % SEG == 0 && 64 * HG / SEG == 16, "16 tokens per store round");
     const int y0 = wh * WIN + g.shift, x0 = ww * WIN + g.shift;
-    char* obase = reinterpret_cast<char*>(a.out) + (size_t)b * g.H * g.W * C * 2 + grp_off;
+    const uint32_t C2 = 2u * C;
+    // window origin as a uniform byte offset; a lane adds its token's (ty W + tx) C2 + 16 c, and
+    // the last window row / column (cyclic shift) subtracts H W C2 / W C2 where it wraps
+    char* obase = reinterpret_cast<char*>(a.out) + (size_t)b * g.H * g.W * C * 2 + grp_off +
+                  (size_t)((uint32_t)y0 * g.W + x0) * C2;
+    const uint32_t rowb = (uint32_t)g.W * C2, imgb = (uint32_t)g.H * rowb;
+    const int ly = g.H - y0, lx = g.W - x0;
+    const bool wrap = ly < WIN || lx < WIN;  // wave-uniform
     // thread s = tid + 64 HG k holds slot c = tid % SEG of token t0 + 16k (64 HG / SEG = 16)
     const int t0 = threadIdx.x / SEG, c = threadIdx.x - t0 * SEG;
-    const uint32_t C2 = 2u * C;
     hvk_u32x4 v[NS];
-    uint32_t off[NS];
+    int off[NS];  // signed: a wrapped token lies BEFORE the window origin (|off| < H W 2C < 2^31)
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       const int t = t0 + 16 * k, ty = t / WIN, tx = t - ty * WIN;
       // slots past the window (last round only) read a valid slab address and store nothing
-      v[k] = lds_rd128<0>(lds_addr(smem) + (t < K::N ? (ty * K::RUN + tx * K::RS + c) * 16 : 0));
-      int y = y0 + ty, x = x0 + tx;
-      y -= y >= g.H ? g.H : 0;
-      x -= x >= g.W ? g.W : 0;
-      const int row = (int)HVK_BCHECK(__umul24((uint32_t)y, (uint32_t)g.W) + x, g.H * g.W);  // in image b
-      off[k] = __umul24((uint32_t)row, C2) + c * 16;  // < 2^32: hvk_wmsa_fwd bounds H W 6C
+      const uint32_t sl = __umul24((uint32_t)ty, (uint32_t)(K::RUN * 16)) + __umul24((uint32_t)tx, (uint32_t)(K::RS * 16));
+      v[k] = lds_rd128<0>(lds_addr(smem) + (t < K::N ? sl + c * 16 : 0u));
+      uint32_t o = mad24(mad24((uint32_t)ty, (uint32_t)g.W, (uint32_t)tx), C2, c * 16u);
+      if (wrap) o -= (ty >= ly ? imgb : 0u) + (tx >= lx ? rowb : 0u);
+      off[k] = (int)o;  // two's complement: the wrapped offsets come out negative
+      (void)HVK_BCHECK(((y0 + ty) % g.H) * g.W + (x0 + tx) % g.W, g.H * g.W);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
       lds_fence(v[k]);
       if (K::N * SEG % (64 * HG) == 0 || t0 + 16 * k < K::N)
-        *reinterpret_cast<uint4*>(obase + off[k]) = u4(v[k]);
+        *reinterpret_cast<uint4*>(obase + (ptrdiff_t)off[k]) = u4(v[k]);
     }
   }
 }
