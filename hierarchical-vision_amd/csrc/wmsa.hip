@@ -655,7 +655,7 @@ __device__ unsigned long long g_bwd_stamps[8];
   } while (0)
 #endif
 
-template <int WIN>
+template <int WIN, bool QNT>
 __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   using K = WinCfg<WIN>;
   using PC = PairCfg<WIN>;
@@ -721,6 +721,9 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 
   // own q, k, dO tiles and all V tiles of a window -> registers (next window: issued after
   // phase A into the registers phase A was the last to read, so the loads hide under phase B)
+  // qkv reads (the saved activation, read once here): nontemporal when QNT, so a qkv larger
+  // than the Infinity Cache does not evict dO and the dqkv this kernel writes for the next GEMMs
+  auto qld = [&](uint32_t off) { return QNT ? hvk_bld16_nt(r_qkv, off) : hvk_bld16(r_qkv, off); };
   uint4 qf[TPW], kf[TPW], df[TPW], vf[NT];
   int rown[TPW];  // own token rows of the next window, -1 = padding
   auto load_window = [&](int w) {
@@ -734,15 +737,15 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
     for (int t = 0; t < NT; ++t) {
       const int tok = 16 * t + lw;
       rt[t] = tok < K::N ? window_token_row(g, b, wh, ww, WIN, tok) : -1;
-      vf[t] = hvk_bld16(r_qkv, rt[t] < 0 ? HVK_OOB : (uint32_t)(rt[t] * C3 + 2 * C + h * 32 + 8 * gq) * 2);
+      vf[t] = qld(rt[t] < 0 ? HVK_OOB : (uint32_t)(rt[t] * C3 + 2 * C + h * 32 + 8 * gq) * 2);
     }
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       rown[j] = 2 * j + 1 < NT ? (hf ? rt[2 * j + 1] : rt[2 * j]) : (hf ? -1 : rt[2 * j]);
       const uint32_t o = rown[j] < 0 ? HVK_OOB : (uint32_t)(rown[j] * C3 + h * 32 + 8 * gq) * 2;
       const uint32_t od = rown[j] < 0 ? HVK_OOB : (uint32_t)(rown[j] * C + h * 32 + 8 * gq) * 2;
-      qf[j] = hvk_bld16(r_qkv, o);
-      kf[j] = hvk_bld16(r_qkv, o + 2 * C);
+      qf[j] = qld(o);
+      kf[j] = qld(o + 2 * C);
       df[j] = hvk_bld16(r_dout, od);
     }
   };
@@ -1104,10 +1107,17 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
     constexpr size_t plds = PairCfg<WIN>::LDS;
     static bool pattr = false;
     if (!pattr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
       pattr = true;
     }
+    // qkv read policy (HVK_WMSA_BWD_NT, A/B runs, read per call): 0 default (cached), 1 always
+    // nontemporal, 2 nontemporal when qkv exceeds the 256 MB Infinity Cache
+    const char* nte = getenv("HVK_WMSA_BWD_NT");
+    const int ntm = nte ? atoi(nte) : 0;
+    const bool qnt = ntm == 1 || (ntm == 2 && (size_t)a.g.B * a.g.H * a.g.W * a.g.C * 6 > ((size_t)256 << 20));
     // buffer descriptors span < 2^31 bytes: launch over batch slices when qkv is larger
     const size_t img_bytes = (size_t)a.g.H * a.g.W * 3 * a.g.C * 2;
     const int per = (int)(((size_t)1 << 31) / img_bytes);
@@ -1123,7 +1133,10 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
       s.dqkv += b0 * tok * 3 * a.g.C;
       const int it = s.g.n_chunks * s.g.nH;
       const int nb = s.g.xcd_runs ? 8 * ((it + 7) / 8) : (s.g.n_chunks + 7) / 8 * 8 * s.g.nH;
-      HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, wmsa_bwd_pair_kernel<WIN>, dim3(nb), dim3(kThreads), plds, st, s);
+      if (qnt)
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, true>), dim3(nb), dim3(kThreads), plds, st, s);
+      else
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, false>), dim3(nb), dim3(kThreads), plds, st, s);
     }
   }
   HVK_CHECK_LAUNCH("wmsa_bwd");
