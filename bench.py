@@ -172,9 +172,8 @@ def stage_breakdown(model, batch, durations_ms, per_elem, backward):
 
 
 def kernel_names(windows):
-    # w <= 8: one workgroup per (window, head group) (wmsa_win.hip); grids of under 2.5 resident
-    # rounds (SwinV2-T stage 3) take the persistent ring form (wmsa_ring.hip)
-    fwd = sorted({f"wmsa_fwd_win_kernel<{w},HG>+ring" if w <= 8 else f"wmsa_fwd_large_kernel<{w}>" for w in windows})
+    # w <= 8: one workgroup per (window, head group) (wmsa_win.hip)
+    fwd = sorted({f"wmsa_fwd_win_kernel<{w},HG>" if w <= 8 else f"wmsa_fwd_large_kernel<{w}>" for w in windows})
     bwd = sorted({f"wmsa_bwd_pair_kernel<{w}>" if w <= 8 else f"wmsa_bwd_large_kernel<{w}>" for w in windows})
     return "+".join(fwd), "+".join(bwd)
 

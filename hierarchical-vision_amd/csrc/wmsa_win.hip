@@ -522,11 +522,13 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
 
 template <int WIN, int HG>
 int launch_win(FwdArgs& a, hipStream_t st) {
-  // a grid of few rounds of resident workgroups ends in a long partial round: there the
-  // persistent ring form is faster (SwinV2-T stage 3: 1.6 rounds, 19.6 vs 21.8 us); the
-  // threshold in rounds is HVK_WMSA_WIN_MIN_ROUNDS (A/B runs), default 2.5
-  const char* mr = getenv("HVK_WMSA_WIN_MIN_ROUNDS");  // per call: the tests force either form
-  const double min_rounds = mr ? atof(mr) : 2.5;
+  // grids under HVK_WMSA_WIN_MIN_ROUNDS rounds of resident workgroups take the persistent ring
+  // form (A/B runs; read per call, the tests force either form).  Default 0, the win form
+  // everywhere: in-step it beats the ring at every SwinV2-T stage, the 1.6-round stage 3
+  // included (19.3 vs 23.8 us; the isolated microbench, from cold caches, had it the other way:
+  // profiles/round3/wmsa_fwd_win/stages_stage3_routing.txt)
+  const char* mr = getenv("HVK_WMSA_WIN_MIN_ROUNDS");
+  const double min_rounds = mr ? atof(mr) : 0.0;
   const int per_cu = (160 * 1024) / RingCfg<WIN, HG>::LDS;
   const double rounds = (double)a.g.n_windows * (a.g.nH / HG) / (256.0 * (per_cu > 0 ? per_cu : 1));
   // per-image byte offsets of the output stores are 32-bit (24-bit multiplies): larger images

@@ -25,7 +25,7 @@ def test_wmsa_work_swinv2_tiny():
 
 def test_kernel_names():
     import bench
-    assert bench.kernel_names({7}) == ("wmsa_fwd_win_kernel<7,HG>+ring", "wmsa_bwd_pair_kernel<7>")
+    assert bench.kernel_names({7}) == ("wmsa_fwd_win_kernel<7,HG>", "wmsa_bwd_pair_kernel<7>")
     f, b = bench.kernel_names({12, 24})
     assert f == "wmsa_fwd_large_kernel<12>+wmsa_fwd_large_kernel<24>"
     assert b == "wmsa_bwd_large_kernel<12>+wmsa_bwd_large_kernel<24>"

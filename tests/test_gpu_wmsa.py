@@ -34,7 +34,7 @@ def _inputs(B, H, W, nh, win, seed, std=1.0):
 
 def _force_form(monkeypatch, form):
     """Windows <= 8: pick the forward form (wmsa_win.hip / wmsa_ring.hip) whatever the grid size
-    (by default grids of few resident rounds take the ring form)."""
+    (HVK_WMSA_WIN_MIN_ROUNDS routes small grids to the ring form when set)."""
     monkeypatch.setenv("HVK_WMSA_FWD_FORM", form)
     monkeypatch.setenv("HVK_WMSA_WIN_MIN_ROUNDS", "0")
 

@@ -14,7 +14,7 @@ import glob
 import json
 import sys
 
-# the forward: wmsa_fwd_win_kernel at stages 0-2, the ring form at stage 3 (all 12 launches)
+# the forward: wmsa_fwd_win_kernel (the ring form when selected for A/B runs)
 KERNELS = {"wmsa_fwd": ("wmsa_fwd_win_kernel", "wmsa_fwd_ring_kernel"), "wmsa_bwd": ("wmsa_bwd_pair_kernel",),
            "mlp_fwd": ("mlp_fwd_kernel",), "mlp_bwd": ("mlp_bwd_kernel",)}  # the last two: fused stage-0 MLP
 
