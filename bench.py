@@ -419,6 +419,16 @@ def main():
             measured_traffic("wmsa_bwd") if default_cfg else None, work["bwd_exp"] if large else None)
         if launches:
             result["roofline_bwd"]["stages"] = stage_breakdown(model.module, args.batch, launches[1], 16, True)
+        if not large:
+            # SURVEY.md §8(d) counts 16 T C backward bytes, an O read included; the w <= 8 backward
+            # recomputes delta = rowsum(P dP) and never reads O, so the bytes it must move are
+            # 14 T C (q, k, v, dO in; dq, dk, dv out): its rate against those, for the record
+            rb = result["roofline_bwd"]
+            moved = work["bwd_bytes"] * 14 // 16
+            gbs = moved * timed_steps / (bw_ms / 1000) / 1e9
+            rb["bytes_moved_per_step"] = moved
+            rb["moved_gbs"] = round(gbs, 1)
+            rb["moved_frac"] = round(gbs / HBM_PEAK_GBS, 4)
         # dense contractions on libhvk's MFMA GEMMs (every Linear but the classifier head):
         # their algorithmic flops (2 M N K per launch, summed by the library) over their
         # dispatch-packet-timed durations
