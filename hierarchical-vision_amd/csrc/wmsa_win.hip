@@ -15,6 +15,7 @@
 // 0.80 memory-only, 0.74 with a stand-in for the math).  The per-window setup the ring kernel
 // amortised (bias table, head bound) overlaps the DMA: its global reads are issued first and
 // waited for by count while the slab is still in flight.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -545,9 +546,14 @@ int launch_win(FwdArgs& a, hipStream_t st) {
 template <int WIN>
 int win_win(FwdArgs& a, hipStream_t st) {
   const int nH = a.g.nH;
-  // HVK_WMSA_WIN_HG (A/B runs): heads per workgroup; default 3 where it divides, else 4 / 2 / 1
-  const char* e = getenv("HVK_WMSA_WIN_HG");
+  // HVK_WMSA_WIN_HG (A/B runs, all head counts) or HVK_WMSA_WIN_HG_<nH> (one head count):
+  // heads per workgroup; default 3 where it divides, else 4 / 2 / 1
+  char name[40];
+  snprintf(name, sizeof name, "HVK_WMSA_WIN_HG_%d", nH);
+  const char* e = getenv(name);
+  if (!e) e = getenv("HVK_WMSA_WIN_HG");
   const int force = e ? atoi(e) : 0;
+  if (force == 8 && nH % 8 == 0) return launch_win<WIN, 8>(a, st);
   if (force == 6 && nH % 6 == 0) return launch_win<WIN, 6>(a, st);
   if (force == 4 && nH % 4 == 0) return launch_win<WIN, 4>(a, st);
   if (force == 2 && nH % 2 == 0) return launch_win<WIN, 2>(a, st);
