@@ -547,7 +547,9 @@ template <int WIN>
 int win_win(FwdArgs& a, hipStream_t st) {
   const int nH = a.g.nH;
   // HVK_WMSA_WIN_HG (A/B runs, all head counts) or HVK_WMSA_WIN_HG_<nH> (one head count):
-  // heads per workgroup; default 3 where it divides, else 4 / 2 / 1
+  // heads per workgroup; default 3 where it divides (SwinV2-T: 3 beat 2, 4, 6, 8 at every
+  // stage), else 2 (SwinV2-B's 4 / 8 / 16 / 32 heads: 0.614 vs 0.595 with 4, one 128-B line
+  // per head pair and part, 7 workgroups per CU: profiles/round3/wmsa_fwd_win/stages_b224_hg2.txt)
   char name[40];
   snprintf(name, sizeof name, "HVK_WMSA_WIN_HG_%d", nH);
   const char* e = getenv(name);
@@ -558,7 +560,6 @@ int win_win(FwdArgs& a, hipStream_t st) {
   if (force == 4 && nH % 4 == 0) return launch_win<WIN, 4>(a, st);
   if (force == 2 && nH % 2 == 0) return launch_win<WIN, 2>(a, st);
   if (nH % 3 == 0) return launch_win<WIN, 3>(a, st);
-  if (nH % 4 == 0) return launch_win<WIN, 4>(a, st);
   if (nH % 2 == 0) return launch_win<WIN, 2>(a, st);
   return launch_win<WIN, 1>(a, st);
 }
