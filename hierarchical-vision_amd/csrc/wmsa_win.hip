@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
           const unsigned off = pre[k % K::KP] + U;
 #if HVK_WIN_PROBE == 2
           (void)off;
-          asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + j * 1024) + 16u * lane),
+          asm volatile("ds_write_b128 %0, %1" ::"v"(lds_addr(smem + j * 1024) + 16u * (threadIdx.x & 63)),
                        "v"(hvk_u32x4{0, 0, 0, 0}) : "memory");
 #else
           dma16_lds<decltype(nt_t)::value>(img, off, lds_addr(smem) + (uint32_t)j * 1024u);
