@@ -4,8 +4,10 @@ The product path has exactly one implementation of every hot op: the HIP
 kernels in this library.  There is no CPU or eager fallback -- if the library
 is missing or a tensor is not on the GPU the call raises.
 """
+import contextlib
 import ctypes
 import os
+import sys
 
 import torch  # noqa: F401  -- must be imported first: libhvk binds to torch's HIP runtime
 
@@ -27,6 +29,8 @@ SIGNATURES = {
     "hvk_kernel_timer_kinds": (_i, [_i]),
     "hvk_kernel_timer_launch": (_i, [_i, _p, _p, _p]),
     "hvk_last_error_string": (ctypes.c_char_p, []),
+    "hvk_set_option": (_i, [ctypes.c_char_p, ctypes.c_longlong, _p]),
+    "hvk_get_option": (_i, [ctypes.c_char_p, _p]),
     "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
@@ -89,7 +93,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 7  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
+ABI_VERSION = 8  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
 
 
 def load():
@@ -118,7 +122,41 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        # A/B runs only: HVK_OPTIONS="name=value,..." sets library options once at load (loudly);
+        # libhvk itself reads no environment variable
+        for item in filter(None, os.environ.get("HVK_OPTIONS", "").split(",")):
+            name, _, value = item.partition("=")
+            set_option(name.strip(), int(value))
+            print(f"[hvamd] libhvk option {name.strip()} = {int(value)} (HVK_OPTIONS)", file=sys.stderr)
     return _lib
+
+
+def set_option(name, value):
+    """Set a libhvk option (include/hvk.h); returns the previous value."""
+    lib = load()
+    prev = ctypes.c_longlong()
+    rc = lib.hvk_set_option(name.encode(), int(value), ctypes.byref(prev))
+    if rc != 0:
+        raise RuntimeError(f"hvk_set_option failed: {lib.hvk_last_error_string().decode(errors='replace')}")
+    return prev.value
+
+
+def get_option(name):
+    lib = load()
+    v = ctypes.c_longlong()
+    if lib.hvk_get_option(name.encode(), ctypes.byref(v)) != 0:
+        raise RuntimeError(f"hvk_get_option failed: {lib.hvk_last_error_string().decode(errors='replace')}")
+    return v.value
+
+
+@contextlib.contextmanager
+def option(name, value):
+    """with option("wmsa_fwd_form", 1): ... -- restores the previous value on exit."""
+    prev = set_option(name, value)
+    try:
+        yield
+    finally:
+        set_option(name, prev)
 
 
 def call(name, *args):

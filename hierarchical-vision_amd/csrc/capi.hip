@@ -1,6 +1,7 @@
 // C-ABI status plumbing for libhvk: error codes + last-error text (thread-local).
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <vector>
 
@@ -20,7 +21,53 @@ int hvk_set_error(int code, const char* fmt, ...) {
 
 const char* hvk_last_error_string(void) { return g_hvk_err; }
 
-int hvk_abi_version(void) { return 7; }
+int hvk_abi_version(void) { return 8; }
+
+}  // extern "C"
+
+namespace {
+struct OptDef {
+  const char* name;
+  long long value, lo, hi;
+};
+OptDef g_opts[HVK_OPT_COUNT] = {
+    {"wmsa_fwd_form", 0, 0, 1},
+    {"wmsa_bwd_nt", 0, 0, 2},
+    {"wmsa_bwd_slice_bytes", 1ll << 31, 1, 1ll << 31},
+    {"gemm_pp", 0, 0, 3},
+    {"tile_wide", -1, -1, 1},
+    {"dw_tile", 5, 4, 8},
+};
+int find_opt(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < HVK_OPT_COUNT; ++i)
+    if (!strcmp(g_opts[i].name, name)) return i;
+  return -1;
+}
+}  // namespace
+
+long long hvk_opt(int id) { return g_opts[id].value; }
+
+extern "C" {
+
+int hvk_set_option(const char* name, long long value, long long* previous) {
+  const int i = find_opt(name);
+  if (i < 0) return hvk_set_error(HVK_EINVAL, "hvk_set_option: unknown option '%s'", name ? name : "(null)");
+  if (value < g_opts[i].lo || value > g_opts[i].hi)
+    return hvk_set_error(HVK_EINVAL, "hvk_set_option: %s = %lld not in [%lld, %lld]", name, value,
+                         g_opts[i].lo, g_opts[i].hi);
+  if (previous) *previous = g_opts[i].value;
+  g_opts[i].value = value;
+  return HVK_OK;
+}
+
+int hvk_get_option(const char* name, long long* value) {
+  const int i = find_opt(name);
+  if (i < 0) return hvk_set_error(HVK_EINVAL, "hvk_get_option: unknown option '%s'", name ? name : "(null)");
+  if (!value) return hvk_set_error(HVK_EINVAL, "hvk_get_option: null pointer");
+  *value = g_opts[i].value;
+  return HVK_OK;
+}
 
 // ---- kernel timer ------------------------------------------------------------------
 namespace {

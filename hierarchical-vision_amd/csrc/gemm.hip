@@ -535,13 +535,8 @@ const LinCfg kLin[][4] = {
 };
 
 const LinCfg* pick(int K, int N) {
-  static const int variant = [] {
-    const char* e = getenv("HVK_LINEAR_VARIANT");
-    const int v = e ? atoi(e) : 0;
-    return v >= 0 && v < 4 ? v : 0;
-  }();
   for (const auto& row : kLin)
-    if (row[0].K == K && row[0].N == N) return &row[variant];
+    if (row[0].K == K && row[0].N == N) return &row[0];
   return nullptr;
 }
 

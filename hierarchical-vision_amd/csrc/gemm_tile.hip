@@ -532,17 +532,10 @@ int launch_pp_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16
 }
 
 // ping-pong tile choice: 0 (default) off, 1 wherever a ping-pong tile divides N, 2 only
-// 256 x 256, 3 only 128 x 384; initial value from HVK_GEMM_PP, changed by hvk_gemm_set_pp
+// 256 x 256, 3 only 128 x 384; option "gemm_pp" (hvk_set_option / hvk_gemm_set_pp
 // (A/B runs and the tests that pin both kernels to the same bits).  Off by default: measured
 // 3-25 % slower than the 128-row tiles on every SwinV2 stage 1-3 shape (tools/bench_pp.py)
-static int g_pp_mode = -1;
-static int gemm_pp_mode() {
-  if (g_pp_mode < 0) {
-    const char* e = getenv("HVK_GEMM_PP");
-    g_pp_mode = e ? atoi(e) : 0;
-  }
-  return g_pp_mode;
-}
+static int gemm_pp_mode() { return (int)hvk_opt(HVK_OPT_GEMM_PP); }
 
 template <int EPI>
 int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2, int M,
@@ -553,14 +546,6 @@ int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16*
   if (N % 256 == 0 && mode != 3) return launch_pp_<EPI, 8, 4>(X, W, bias, Y, Y2, M, N, K, st);
   if (N % 384 == 0 && mode != 2) return launch_pp_<EPI, 4, 6>(X, W, bias, Y, Y2, M, N, K, st);
   return -1;
-}
-
-static bool tile_pipe() {
-  static const int v = [] {
-    const char* e = getenv("HVK_TILE_PIPE");
-    return e ? atoi(e) : 1;
-  }();
-  return v != 0;
 }
 
 template <int EPI, bool PIPE, int TN>
@@ -588,11 +573,8 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
                 int M, int N, int K, hipStream_t st) {
   // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1536 case
   // (tools/bench_gemm.py, interleaved: 3-25 % faster on the stage-2/3 shapes, 6 % slower on
-  // the stage-2 projection); HVK_TILE_WIDE=0 / 1 forces 128 / 192 columns where both divide N
-  static const int force = [] {
-    const char* e = getenv("HVK_TILE_WIDE");
-    return e ? atoi(e) : -1;
-  }();
+  // the stage-2 projection); option "tile_wide" 0 / 1 forces 128 / 192 columns where both divide N
+  const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
   {
     const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
     if (r >= 0) return r;
@@ -604,10 +586,8 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   const bool wide = N % TileCfg<6>::BN == 0 &&
                     (force >= 0 ? force == 1 : ((N > 384 || K >= 1536) && !epi1_narrow));
   if (N % TileCfg<4>::BN == 0 && !wide)
-    return tile_pipe() ? launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st)
-                       : launch_tile_<EPI, false, 4>(X, W, bias, Y, Y2, M, N, K, st);
-  return tile_pipe() ? launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st)
-                     : launch_tile_<EPI, false, 6>(X, W, bias, Y, Y2, M, N, K, st);
+    return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st);
+  return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st);
 }
 
 }  // namespace
@@ -623,9 +603,9 @@ int hvk_gemm_probe_read(void* dst, int nblocks) {
 
 int hvk_gemm_set_pp(int mode) {
   if (mode < 0 || mode > 3) return hvk_set_error(HVK_EINVAL, "hvk_gemm_set_pp: mode %d not in 0..3", mode);
-  const int prev = gemm_pp_mode();
-  g_pp_mode = mode;
-  return prev;
+  long long prev = 0;
+  hvk_set_option("gemm_pp", mode, &prev);
+  return (int)prev;
 }
 
 int hvk_gemm_supported(int M, int K, int N) {

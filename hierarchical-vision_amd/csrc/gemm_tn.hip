@@ -255,11 +255,7 @@ struct Plan {
 };
 
 int tile_variant() {
-  static const int v = [] {
-    const char* e = getenv("HVK_DW_TILE");
-    return e ? atoi(e) : (int)V_T8A;
-  }();
-  return v;
+  return (int)hvk_opt(HVK_OPT_DW_TILE);
 }
 
 bool plan(int M, int N, int K, Plan& p) {

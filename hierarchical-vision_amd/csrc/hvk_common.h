@@ -23,6 +23,26 @@ int hvk_set_error(int code, const char* fmt, ...);
 }
 #endif
 
+// ---- library options (capi.hip): a fixed table set only through hvk_set_option (include/hvk.h);
+// libhvk reads no environment variable.  Each option that changes a result has a GPU test.
+enum HvkOption {
+  HVK_OPT_WMSA_FWD_FORM = 0,    // w <= 8 forward: 0 one workgroup per (window, head group), 1 ring
+  HVK_OPT_WMSA_BWD_NT,          // w <= 8 backward qkv reads: 0 cached, 1 nontemporal, 2 nt past 256 MB
+  HVK_OPT_WMSA_BWD_SLICE_BYTES, // w <= 8 backward: batch slice so one launch's qkv stays below this
+  HVK_OPT_GEMM_PP,              // tiled GEMM: 0 128-row tiles, 1 ping-pong 256x256 / 128x384, 2 / 3 one of them
+  HVK_OPT_TILE_WIDE,            // tiled GEMM: -1 by shape, 0 128-column, 1 192-column tiles
+  HVK_OPT_DW_TILE,              // weight gradient, 192-multiple shapes: tile variant 4..8
+  HVK_OPT_COUNT
+};
+long long hvk_opt(int id);
+#ifdef __cplusplus
+extern "C" {
+#endif
+int hvk_set_option(const char* name, long long value, long long* previous);
+#ifdef __cplusplus
+}
+#endif
+
 #define HVK_OK 0
 #define HVK_EINVAL 1
 #define HVK_EUNSUPPORTED 2

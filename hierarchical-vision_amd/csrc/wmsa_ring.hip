@@ -457,13 +457,6 @@ int launch_ring(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipSt
 template <int WIN>
 int ring_win(FwdArgs& a, int B, int H, int W, int C, int nH, int shift, hipStream_t st) {
   // head group: HG heads per workgroup (the group's q/k/v slices are HG*64 contiguous bytes)
-  static const int force = [] {
-    const char* e = getenv("HVK_WMSA_FWD_HG");
-    return e ? atoi(e) : 0;
-  }();
-  if (force == 4 && nH % 4 == 0) return launch_ring<WIN, 4>(a, B, H, W, C, nH, shift, st);
-  if (force == 3 && nH % 3 == 0) return launch_ring<WIN, 3>(a, B, H, W, C, nH, shift, st);
-  if (force == 2 && nH % 2 == 0) return launch_ring<WIN, 2>(a, B, H, W, C, nH, shift, st);
   // 4 heads per workgroup from 12 heads up (stages 2-3 of SwinV2-T: 3 % faster there, where
   // each workgroup owns only a few windows), else 3
   if (nH % 4 == 0 && nH >= 12) return launch_ring<WIN, 4>(a, B, H, W, C, nH, shift, st);

@@ -505,14 +505,12 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
   a.fd_groups = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nH / HG));
   a.fd_img = hvk_wmsa::make_fastdiv((uint32_t)(a.g.nWh * a.g.nWw));
   a.fd_ww = hvk_wmsa::make_fastdiv((uint32_t)a.g.nWw);
-  // slab DMA cache policy (HVK_WMSA_WIN_NT, A/B runs): 2 (default) nontemporal only when qkv
+  // slab DMA cache policy: nontemporal only when qkv
   // exceeds the 256 MB Infinity Cache -- the qkv GEMM just wrote it, so a smaller one is read
   // from the cache (SwinV2-T stages 1-3; stage 0's 462 MB streams nontemporally): in-step
   // 0.630-0.632 of 8 TB/s vs 0.610 always nontemporal vs 0.570 never (one box,
-  // profiles/round3/wmsa_fwd_win/ab_dma_policy.txt); 1 always, 0 never
-  const char* nt = getenv("HVK_WMSA_WIN_NT");
-  const int ntm = nt ? atoi(nt) : 2;
-  a.dma_nt = ntm == 2 ? ((long long)a.g.B * a.g.H * a.g.W * a.g.C * 6 > (256ll << 20)) : ntm != 0;
+  // profiles/round3/wmsa_fwd_win/ab_dma_policy.txt)
+  a.dma_nt = (long long)a.g.B * a.g.H * a.g.W * a.g.C * 6 > (256ll << 20);
   const long long grid = (items + 7) / 8 * 8;
   if (grid > 0x7fffffffLL) return hvk_set_error(HVK_EINVAL, "wmsa win: %lld windows x groups", items);
   HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_FWD, (wmsa_fwd_win_kernel<WIN, HG, LSE, MM>), dim3((unsigned)grid), dim3(64 * HG),
@@ -523,19 +521,13 @@ int launch_win_(FwdArgs& a, hipStream_t st) {
 
 template <int WIN, int HG>
 int launch_win(FwdArgs& a, hipStream_t st) {
-  // grids under HVK_WMSA_WIN_MIN_ROUNDS rounds of resident workgroups take the persistent ring
-  // form (A/B runs; read per call, the tests force either form).  Default 0, the win form
-  // everywhere: in-step it beats the ring at every SwinV2-T stage, the 1.6-round stage 3
-  // included (19.3 vs 23.8 us; the isolated microbench, from cold caches, had it the other way:
-  // profiles/round3/wmsa_fwd_win/stages_stage3_routing.txt)
-  const char* mr = getenv("HVK_WMSA_WIN_MIN_ROUNDS");
-  const double min_rounds = mr ? atof(mr) : 0.0;
-  const int per_cu = (160 * 1024) / RingCfg<WIN, HG>::LDS;
-  const double rounds = (double)a.g.n_windows * (a.g.nH / HG) / (256.0 * (per_cu > 0 ? per_cu : 1));
+  // the win form everywhere: in-step it beats the persistent ring at every SwinV2-T stage, the
+  // 1.6-round stage 3 included (19.3 vs 23.8 us; the isolated microbench, from cold caches, had
+  // it the other way: profiles/round3/wmsa_fwd_win/stages_stage3_routing.txt)
   // per-image byte offsets of the output stores are 32-bit (24-bit multiplies): larger images
   // take the ring form, which addresses with 64-bit offsets
   const bool big = a.g.H * a.g.W >= (1 << 24);  // (hvk_wmsa_fwd bounds H W 6C below 2^32)
-  if (rounds < min_rounds || big)
+  if (big)
     return hvk_wmsa::ring_fwd(a, a.g.B, a.g.H, a.g.W, a.g.C, a.g.nH, WIN, a.g.shift, st);
   if (a.g.shift == 0) return a.lse ? launch_win_<WIN, HG, true, 0>(a, st) : launch_win_<WIN, HG, false, 0>(a, st);
   if constexpr (WIN == 7)
@@ -546,19 +538,9 @@ int launch_win(FwdArgs& a, hipStream_t st) {
 template <int WIN>
 int win_win(FwdArgs& a, hipStream_t st) {
   const int nH = a.g.nH;
-  // HVK_WMSA_WIN_HG (A/B runs, all head counts) or HVK_WMSA_WIN_HG_<nH> (one head count):
-  // heads per workgroup; default 3 where it divides (SwinV2-T: 3 beat 2, 4, 6, 8 at every
-  // stage), else 2 (SwinV2-B's 4 / 8 / 16 / 32 heads: 0.614 vs 0.595 with 4, one 128-B line
-  // per head pair and part, 7 workgroups per CU: profiles/round3/wmsa_fwd_win/stages_b224_hg2.txt)
-  char name[40];
-  snprintf(name, sizeof name, "HVK_WMSA_WIN_HG_%d", nH);
-  const char* e = getenv(name);
-  if (!e) e = getenv("HVK_WMSA_WIN_HG");
-  const int force = e ? atoi(e) : 0;
-  if (force == 8 && nH % 8 == 0) return launch_win<WIN, 8>(a, st);
-  if (force == 6 && nH % 6 == 0) return launch_win<WIN, 6>(a, st);
-  if (force == 4 && nH % 4 == 0) return launch_win<WIN, 4>(a, st);
-  if (force == 2 && nH % 2 == 0) return launch_win<WIN, 2>(a, st);
+  // heads per workgroup: 3 where it divides (SwinV2-T: 3 beat 2, 4, 6, 8 at every stage), else 2
+  // (SwinV2-B's 4 / 8 / 16 / 32 heads: 0.614 vs 0.595 with 4, one 128-B line per head pair and
+  // part, 7 workgroups per CU: profiles/round3/wmsa_fwd_win/stages_b224_hg2.txt)
   if (nH % 3 == 0) return launch_win<WIN, 3>(a, st);
   if (nH % 2 == 0) return launch_win<WIN, 2>(a, st);
   return launch_win<WIN, 1>(a, st);

@@ -38,6 +38,9 @@ class GradientBuckets:
         # all-reduce / synchronize path on a one-GPU box, tests/test_gpu_ddp.py)
         self.enabled = self.world > 1 or (force and dist.is_initialized())
         self.defer = False  # graph mode: no hook-launched all-reduce (allreduce_now() instead)
+        # grad_accum: microbatches before the last only accumulate into the bucket views (no
+        # arrival count, no all-reduce: composer's DDP no_sync)
+        self.accumulating = False
         self.buckets = []
         self._hooks = []
         if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
@@ -79,6 +82,8 @@ class GradientBuckets:
             if p.grad is not v:  # the fresh gradient autograd handed over -> its bucket slot
                 v.copy_(p.grad)
                 p.grad = v
+            if self.accumulating:  # later microbatches add onto the view in place
+                return
             self._pending[bi] -= 1
             if self._pending[bi] == 0 and self.enabled and not self.defer:
                 flat = self.buckets[bi][0]

@@ -17,9 +17,35 @@ from .algorithmic import Event, State
 from .ddp import GradientBuckets
 
 
+def resolve_grad_accum(grad_accum, device_type):
+    """composer's `grad_accum` as main.py passes it (main.py:38-41, :121): "auto" needs a GPU
+    (the same ValueError on CPU) and resolves to 1 here -- composer's "auto" only shrinks the
+    microbatch after a CUDA OOM, and a bs256 SwinV2 step uses a small part of 288 GB of HBM;
+    otherwise a positive integer number of microbatches per batch."""
+    if grad_accum == "auto":
+        if device_type != "cuda":
+            raise ValueError('grad_accum="auto" requires training with a GPU; please specify '
+                             'grad_accum as an integer')
+        return 1
+    if isinstance(grad_accum, bool) or not isinstance(grad_accum, int) or grad_accum < 1:
+        raise ValueError(f"grad_accum must be 'auto' or a positive integer, got {grad_accum!r}")
+    return grad_accum
+
+
+def _split_batch(batch, n):
+    """The batch's tensors cut into n equal microbatches along dim 0 (composer's
+    `_default_split_batch` for a tuple/list batch)."""
+    size = batch[0].shape[0]
+    if size % n:
+        raise ValueError(f"batch of {size} samples does not split into grad_accum={n} "
+                         "equal microbatches")
+    return [type(batch)(t.narrow(0, i * (size // n), size // n) for t in batch)
+            for i in range(n)]
+
+
 class Trainer:
     def __init__(self, model, optimizer, algorithms=(), bucket_mb=64.0, dtype=torch.bfloat16,
-                 device_transforms=None):
+                 device_transforms=None, grad_accum=1):
         self.model = model
         self.optimizer = optimizer
         self.algorithms = list(algorithms)
@@ -33,6 +59,8 @@ class Trainer:
                 self.device_transforms = None
         self.state = State(model, optimizer)
         self.buckets = GradientBuckets(model, bucket_mb=bucket_mb)
+        dev = next(model.parameters()).device.type
+        self.grad_accum = resolve_grad_accum(grad_accum, dev)
         self._run(Event.INIT)
 
     def _run(self, event):
@@ -44,22 +72,39 @@ class Trainer:
         st = self.state
         if self.device_transforms is not None:
             batch = self.device_transforms(batch)
-        st.batch = batch
+        # every .grad None and the arrival counts re-armed before the backward: after a
+        # capture()/replay() .grad still points at the graph's gradient tensors, which autograd
+        # would otherwise accumulate this step's gradient onto
+        self.buckets.reset()
         self.model.train()
         dev_type = batch[0].device.type
-        with torch.autocast(device_type=dev_type, dtype=self.dtype, enabled=dev_type == "cuda"):
-            st.outputs = self.model(st.batch)
-        self._run(Event.BEFORE_LOSS)
-        st.loss = self.model.loss(st.outputs, st.batch)
-        self._run(Event.AFTER_LOSS)
-        st.loss.backward()
+        micro = _split_batch(batch, self.grad_accum) if self.grad_accum > 1 else [batch]
+        total = None
+        for i, mb in enumerate(micro):
+            # composer's microbatch loop: each microbatch's loss scaled by its share of the
+            # batch, gradients accumulated; the all-reduce hooks fire on the last one only
+            # (DDP no_sync for the others)
+            self.buckets.accumulating = i < len(micro) - 1
+            st.batch = mb
+            with torch.autocast(device_type=dev_type, dtype=self.dtype, enabled=dev_type == "cuda"):
+                st.outputs = self.model(st.batch)
+            self._run(Event.BEFORE_LOSS)
+            st.loss = self.model.loss(st.outputs, st.batch)
+            self._run(Event.AFTER_LOSS)
+            if len(micro) > 1:
+                st.loss = st.loss * (1.0 / len(micro))
+            st.loss.backward()
+            total = st.loss.detach() if total is None else total + st.loss.detach()
+        self.buckets.accumulating = False
+        st.batch = batch
+        st.loss = total
         self._grad_mean()
         self._run(Event.AFTER_BACKWARD)
         self.optimizer.step()
         self.buckets.reset()
         st.timestamp_batch += 1
         self._run(Event.BATCH_END)
-        return st.loss.detach()
+        return st.loss
 
     def _grad_mean(self, wait=True):
         """Bucket all-reduces done -> mean gradients: handed to the optimizer as a scale when it
@@ -97,6 +142,9 @@ class Trainer:
     def capture(self, batch, warmup=3):
         """Warm up on a side stream (allocations, library init, optimizer state), then
         capture the backward graph and the update graph."""
+        if self.grad_accum != 1:
+            raise NotImplementedError("graph mode captures one microbatch per step; "
+                                      "use train_step() for grad_accum > 1")
         # drop every reference to earlier autograd graphs (outputs / loss of eager steps):
         # their AccumulateGrad nodes are bound to the stream they ran on, and a backward on
         # the capture stream that reuses them would synchronise with it and break capture

@@ -30,6 +30,22 @@ extern "C" {
 int hvk_abi_version(void);
 const char* hvk_last_error_string(void);
 
+/* ---- Library options -------------------------------------------------------------------
+ * libhvk reads no environment variable: the few selectable forms are a fixed table of named
+ * integer options, changed only here (A/B runs and the parity tests that pin alternate forms to
+ * the default one).  set returns HVK_EINVAL for an unknown name or a value outside its range and
+ * stores the old value in *previous when that is not NULL.
+ *   wmsa_fwd_form         0 (default) one workgroup per (window, head group), 1 persistent ring
+ *   wmsa_bwd_nt           w <= 8 backward qkv reads: 0 (default) cached, 1 nontemporal, 2 nt when
+ *                         qkv exceeds the 256 MB Infinity Cache
+ *   wmsa_bwd_slice_bytes  w <= 8 backward: launch over batch slices whose qkv stays below this
+ *                         (default 2^31, the buffer-descriptor range)
+ *   gemm_pp               tiled GEMM kernel choice (hvk_gemm_set_pp below), default 0
+ *   tile_wide             tiled GEMM: -1 (default) tile width by shape, 0 128, 1 192 columns
+ *   dw_tile               weight gradient at 192-multiple shapes: tile variant 4..8 (default 5) */
+int hvk_set_option(const char* name, long long value, long long* previous);
+int hvk_get_option(const char* name, long long* value);
+
 /* ---- Kernel timer (measurement only; bench.py's roofline) ---------------------------
  * enable(n > 0): time the next n launches of the timed kernels (kind 0 = W-MSA forward,
  * 1 = W-MSA backward main kernel, 2 = forward / input-gradient GEMMs, 3 = weight-gradient
@@ -151,7 +167,7 @@ int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, in
  * 128 x 192 two-workgroups-per-CU kernel only, 1 = the ping-pong 256 x 256 / 128 x 384 kernel
  * (one 8-wave workgroup per CU) wherever its tile divides N, 2 / 3 = only its 256 x 256 /
  * 128 x 384 tile.  Both kernels accumulate in the same order, so their results are
- * bit-identical.  Returns the previous mode (initially $HVK_GEMM_PP, else 0). */
+ * bit-identical.  Returns the previous mode (option "gemm_pp", initially 0). */
 int hvk_gemm_set_pp(int mode);
 
 /* ---- Weight-gradient GEMM (the backward of every SwinV2 Linear) ----------------------

@@ -24,7 +24,17 @@ static int g_fail = 0;
 static void* const P = reinterpret_cast<void*>(0x1000);
 
 int main() {
-  EXPECT(hvk_abi_version() == 7);
+  EXPECT(hvk_abi_version() == 8);
+
+  // options: unknown names and out-of-range values refused, set/get round trip
+  long long prev = -7, v = -7;
+  EXPECT(hvk_set_option("no_such_option", 0, nullptr) == HVK_EINVAL);
+  EXPECT(hvk_set_option(nullptr, 0, nullptr) == HVK_EINVAL);
+  EXPECT(hvk_set_option("wmsa_fwd_form", 2, nullptr) == HVK_EINVAL);
+  EXPECT(hvk_get_option("wmsa_fwd_form", nullptr) == HVK_EINVAL);
+  EXPECT(hvk_set_option("wmsa_fwd_form", 1, &prev) == HVK_OK && prev == 0);
+  EXPECT(hvk_get_option("wmsa_fwd_form", &v) == HVK_OK && v == 1);
+  EXPECT(hvk_set_option("wmsa_fwd_form", 0, nullptr) == HVK_OK);
 
   // W-MSA: null pointers, head_dim != 32, window not built, indivisible maps, short workspace
   EXPECT(hvk_wmsa_fwd(nullptr, nullptr, nullptr, nullptr, nullptr, 1, 7, 7, 96, 3, 7, 0, nullptr) == HVK_EINVAL);
@@ -34,8 +44,14 @@ int main() {
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 10, 10, 96, 3, 5, 0, nullptr) == HVK_EUNSUPPORTED);
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 15, 15, 96, 3, 7, 3, nullptr) == HVK_EINVAL);
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 14, 14, 96, 3, 7, 7, nullptr) == HVK_EINVAL);
-  // w <= 8: one image's qkv past 32-bit byte offsets (7168^2 tokens x 6C) -> refused, no launch
+  // one image's qkv past 32-bit byte offsets (7168^2 tokens x 6C) -> refused, no launch, for the
+  // w <= 8 forms and the large-window ones, forward and backward
   EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 7168, 7168, 96, 3, 7, 3, nullptr) == HVK_EUNSUPPORTED);
+  EXPECT(hvk_wmsa_fwd(P, P, nullptr, F, F, 1, 7176, 7176, 96, 3, 24, 12, nullptr) == HVK_EUNSUPPORTED);
+  EXPECT(hvk_wmsa_bwd(P, P, nullptr, nullptr, P, nullptr, F, F, F, F, F, hvk_wmsa_bwd_workspace_bytes(3, 24),
+                      1, 7176, 7176, 96, 3, 24, 12, nullptr) == HVK_EUNSUPPORTED);
+  EXPECT(hvk_wmsa_bwd(P, P, nullptr, nullptr, P, nullptr, F, F, F, F, F, hvk_wmsa_bwd_workspace_bytes(3, 7),
+                      1, 7168, 7168, 96, 3, 7, 3, nullptr) == HVK_EUNSUPPORTED);
   for (int w : {4, 6, 7, 8, 12, 16, 24})
     for (int nh = 1; nh <= 32; ++nh) {
       const size_t ws = hvk_wmsa_bwd_workspace_bytes(nh, w);

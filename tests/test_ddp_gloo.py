@@ -132,7 +132,7 @@ class _OracleSwin(torch.nn.Module):
                                         t.tier_base, self.lam)
 
 
-def _train(rank, world, port, out, clip, steps=2, clip_type="norm"):
+def _train(rank, world, port, out, clip, steps=2, clip_type="norm", grad_accum=1):
     from hvamd.algorithmic import EMA, GradientClipping
     from hvamd.hierarchy import Taxonomy
     from hvamd.optim import DecoupledSGDW, set_weight_decay
@@ -145,7 +145,8 @@ def _train(rank, world, port, out, clip, steps=2, clip_type="norm"):
     model = _OracleSwin(tax)
     opt = DecoupledSGDW(set_weight_decay(model), lr=0.05, momentum=0.9, weight_decay=5e-4)
     ema = EMA(half_life="4ba", update_interval="1ba")
-    trainer = Trainer(model, opt, [GradientClipping(clip_type, clip), ema], bucket_mb=0.05)
+    trainer = Trainer(model, opt, [GradientClipping(clip_type, clip), ema], bucket_mb=0.05,
+                      grad_accum=grad_accum)
     if world > 1:
         assert len(trainer.buckets.buckets) > 2  # several all-reduces in flight in the backward
     g = torch.Generator().manual_seed(7)
@@ -176,3 +177,42 @@ def test_trainer_world2_equals_single_process_full_batch(clip_type, clip):
     for r in range(2):
         for a, b in zip(out[r][0] + out[r][1], single[0][0] + single[0][1]):
             assert torch.allclose(torch.from_numpy(a), torch.from_numpy(b), rtol=1e-4, atol=1e-6), r
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_grad_accum_microbatches_equal_one_batch(world):
+    """grad_accum = 2 (main.py:121 -> composer's microbatch loop: each microbatch's loss scaled
+    by its share, gradients accumulated, DDP's all-reduce only after the last microbatch):
+    parameters and EMA weights after two steps equal one process stepping on the whole batch
+    with grad_accum = 1.  With two gloo ranks the hook-driven bucket all-reduce must fire once
+    per step, after the second microbatch."""
+    single = {}
+    _train(0, 1, 0, single, 0.5, 2, "norm")
+    if world == 1:
+        out = {}
+        _train(0, 1, 0, out, 0.5, 2, "norm", 2)
+    else:
+        out = mp.Manager().dict()
+        mp.spawn(_train, args=(2, _free_port(), out, 0.5, 2, "norm", 2), nprocs=2, join=True)
+    for r in range(world):
+        for a, b in zip(out[r][0] + out[r][1], single[0][0] + single[0][1]):
+            assert torch.allclose(torch.from_numpy(a), torch.from_numpy(b), rtol=1e-4, atol=1e-6), r
+
+
+def test_grad_accum_validation():
+    """main.py:38-41: "auto" without a GPU is the reference's ValueError; "auto" on the GPU
+    resolves to 1; anything but a positive integer raises; a batch that does not split into
+    grad_accum equal microbatches raises."""
+    from hvamd.trainer import _split_batch, resolve_grad_accum
+    with pytest.raises(ValueError, match="requires training with a GPU"):
+        resolve_grad_accum("auto", "cpu")
+    assert resolve_grad_accum("auto", "cuda") == 1
+    assert resolve_grad_accum(4, "cpu") == 4
+    for bad in (0, -1, 1.5, "2", True):
+        with pytest.raises(ValueError):
+            resolve_grad_accum(bad, "cpu")
+    x, y = torch.arange(12.0).view(6, 2), torch.arange(6)
+    parts = _split_batch((x, y), 3)
+    assert [tuple(p[1].tolist()) for p in parts] == [(0, 1), (2, 3), (4, 5)]
+    with pytest.raises(ValueError, match="equal microbatches"):
+        _split_batch((x, y), 4)

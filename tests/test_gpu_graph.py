@@ -107,3 +107,30 @@ def test_eager_step_after_capture_takes_current_lr():
     torch.cuda.synchronize()
     for (n, p), b in zip(model_b.named_parameters(), before):
         assert torch.equal(b, p.detach()), n
+
+
+def test_eager_step_after_replay_matches_eager_trainer():
+    """An eager train_step after capture()/replay() computes this step's gradient alone: the
+    captured gradient tensors .grad still points at must not be accumulated onto.
+    Parameters AND momentum buffers after one more eager step at a nonzero lr equal those of
+    a trainer that only ever stepped eagerly."""
+    tax, model, dev = _setup()
+    model_b = copy.deepcopy(model)
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(4, 3, 56, 56, device=dev, generator=g)
+    y = torch.tensor(tax.leaf_paths[[1, 5, 9, 11]], device=dev)
+    ta, tb = _trainer(model), _trainer(model_b)
+    for _ in range(5):
+        ta.train_step((x, y))
+    tb.capture((x, y), warmup=3)
+    tb.replay()
+    tb.train_step((x, y))
+    torch.cuda.synchronize()
+    pairs = list(zip(model.named_parameters(), model_b.named_parameters()))
+    for (na, pa), (_, pb) in pairs:
+        rel = ((pa - pb).norm() / pa.norm().clamp_min(1e-12)).item()
+        assert rel < 1e-2, (na, rel)
+        ma = ta.optimizer.state[pa]["momentum_buffer"]
+        mb = tb.optimizer.state[pb]["momentum_buffer"]
+        rel = ((ma - mb).norm() / ma.norm().clamp_min(1e-12)).item()
+        assert rel < 5e-2, ("momentum", na, rel)

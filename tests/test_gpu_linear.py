@@ -160,6 +160,25 @@ def test_gemm_tile_matches_fp32(M, K, N, with_bias):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (12544, 768, 768), (1000, 576, 384)])
+def test_gemm_tile_widths_bit_identical(M, K, N):
+    """Where both tile widths divide N, the 128- and 192-column tiles (library option tile_wide)
+    accumulate every output in the same k order: bit-identical outputs."""
+    from hvamd import _lib
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + K + N)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    out = {}
+    for wide in (0, 1):
+        with _lib.option("tile_wide", wide):
+            y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), M, K, N, _lib.stream())
+            torch.cuda.synchronize()
+        out[wide] = y
+    assert torch.equal(out[0].view(torch.int16), out[1].view(torch.int16))
+
+
 @pytest.mark.parametrize("N", [384, 256, 192])
 def test_gemm_tile_sparse_pattern_pins_layout(N):
     """One nonzero token row and one nonzero weight row: the output must be exactly one

@@ -41,6 +41,28 @@ def test_weight_grad_matches_fp32(N, K, M, with_db):
         assert (db - rb).abs().max().item() <= 1e-4 * M ** 0.5 * 4
 
 
+@pytest.mark.parametrize("tile", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("N,K,M", [(1152, 384, 1568), (768, 3072, 2048), (384, 768, 1568)])
+def test_weight_grad_tile_variants_match_fp32(tile, N, K, M):
+    """Every selectable tile variant of the 192-multiple shapes (library option dw_tile, the
+    default is 5) against the fp32 reference; variants that do not fit a shape fall back."""
+    from hvamd import _lib
+    lib = _lib.load()
+    gen = torch.Generator(device="cuda").manual_seed(N + K + M + tile)
+    g = torch.randn(M, N, device="cuda", generator=gen).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=gen).bfloat16()
+    with _lib.option("dw_tile", tile):
+        dw = torch.full((N, K), float("nan"), device="cuda")
+        db = torch.full((N,), float("nan"), device="cuda")
+        ws = torch.empty(lib.hvk_weight_grad_workspace(M, N, K), device="cuda", dtype=torch.uint8)
+        _lib.call("hvk_weight_grad", _lib.ptr(g), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db), M, N, K,
+                  _lib.ptr(ws), ws.numel(), _lib.stream())
+        torch.cuda.synchronize()
+    rw, rb = _ref(g, x)
+    assert (dw - rw).abs().max().item() <= 1e-4 * M ** 0.5 * 4
+    assert (db - rb).abs().max().item() <= 1e-4 * M ** 0.5 * 4
+
+
 def test_weight_grad_sparse_pattern_pins_layout():
     """One nonzero token row per operand: dW must be the outer product at exactly the right
     (n, k) and db the g row -- catches transposed or permuted output layouts."""

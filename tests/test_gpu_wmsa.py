@@ -33,10 +33,18 @@ def _inputs(B, H, W, nh, win, seed, std=1.0):
 
 
 def _force_form(monkeypatch, form):
-    """Windows <= 8: pick the forward form (wmsa_win.hip / wmsa_ring.hip) whatever the grid size
-    (HVK_WMSA_WIN_MIN_ROUNDS routes small grids to the ring form when set)."""
-    monkeypatch.setenv("HVK_WMSA_FWD_FORM", form)
-    monkeypatch.setenv("HVK_WMSA_WIN_MIN_ROUNDS", "0")
+    """Windows <= 8: pick the forward form (wmsa_win.hip / wmsa_ring.hip) through the library
+    option "wmsa_fwd_form" (the autouse fixture below restores the defaults)."""
+    import hvamd._lib as lib
+    lib.set_option("wmsa_fwd_form", 1 if form == "ring" else 0)
+
+
+@pytest.fixture(autouse=True)
+def _reset_options():
+    yield
+    import hvamd._lib as lib
+    for name, v in (("wmsa_fwd_form", 0), ("wmsa_bwd_nt", 0), ("wmsa_bwd_slice_bytes", 1 << 31)):
+        lib.set_option(name, v)
 
 
 @pytest.mark.parametrize("form", ["win", "ring"])
@@ -180,7 +188,7 @@ SMALL_CASES = [c for c in CASES if c[4] <= 8]
 @pytest.mark.parametrize("B,H,W,nh,win,shift", SMALL_CASES)
 def test_wmsa_forward_forms_bit_identical(monkeypatch, B, H, W, nh, win, shift, inputs):
     """Windows <= 8 have two forward forms with the same math: one workgroup per (window, head
-    group) (the default, wmsa_win.hip) and the persistent slab ring (HVK_WMSA_FWD_FORM=ring,
+    group) (the default, wmsa_win.hip) and the persistent slab ring (option wmsa_fwd_form = 1,
     wmsa_ring.hip).  Outputs and the optional per-query row constants (lse) agree bit for bit,
     on random inputs and on the scale-100 anti-aligned ones that take the row-max slow path;
     the oracle comparisons above run the default form."""
@@ -211,6 +219,39 @@ def test_wmsa_forward_forms_bit_identical(monkeypatch, B, H, W, nh, win, shift, 
         if keep:
             assert torch.isfinite(lw).all() and torch.equal(lw, lr)
     assert torch.equal(res["win", False][0].view(torch.int16), res["win", True][0].view(torch.int16))
+
+
+@pytest.mark.parametrize("B,H,W,nh,win,shift", [(5, 14, 14, 2, 7, 3), (3, 28, 28, 6, 7, 0),
+                                                (4, 16, 16, 2, 8, 4)])
+def test_wmsa_backward_slices_and_nontemporal_reads_agree(B, H, W, nh, win, shift):
+    """The w <= 8 backward's other launch paths give the default path's bits: the batch-slice
+    loop (taken when qkv exceeds the 2 GiB buffer-descriptor range; here forced with option
+    wmsa_bwd_slice_bytes at 1, 2 and 3 images per slice) and the nontemporal qkv reads
+    (wmsa_bwd_nt = 1).  dqkv is written without atomics, so it must match bit for bit; the
+    CPB-table / scale / q_bias gradients sum per-workgroup atomics in launch order, so they are
+    compared at 1e-5."""
+    import hvamd._lib as lib
+    import hvamd.ops as ops
+    qkv, tab, scale = _inputs(B, H, W, nh, win, 9)
+    gout = torch.from_numpy(np.random.default_rng(10).standard_normal((B, H * W, 32 * nh)).astype(np.float32))
+
+    def run():
+        q = qkv.cuda().bfloat16().requires_grad_(True)
+        t, s = tab.cuda().requires_grad_(True), scale.cuda().requires_grad_(True)
+        qb = torch.zeros(32 * nh, device="cuda", requires_grad=True)
+        ops.window_attention_core(q, t, s, H, W, nh, win, shift, q_bias=qb).backward(gout.cuda().bfloat16())
+        torch.cuda.synchronize()
+        return [x.grad.float().cpu() for x in (q, t, s, qb)]
+
+    base = run()
+    img = H * W * 3 * 32 * nh * 2
+    variants = [("wmsa_bwd_slice_bytes", k * img + 17) for k in (1, 2, 3)] + [("wmsa_bwd_nt", 1)]
+    for name, v in variants:
+        with lib.option(name, v):
+            got = run()
+        assert torch.equal(got[0], base[0]), (name, v)
+        for a, b in zip(got[1:], base[1:]):
+            assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 1e-5, (name, v)
 
 
 def test_wmsa_rejects_unsupported_head_dim():

@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib.SIGNATURES), set(declared) ^ set(_lib.SIGNATURES)
     lib = _lib.load()
-    assert lib.hvk_abi_version() == 7
+    assert lib.hvk_abi_version() == 8
     # [accumulators][dscale nH][dq_bias 32 nH] floats
     assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
     assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4
@@ -46,6 +46,28 @@ def test_library_rejects_bad_arguments_without_gpu():
     assert rc == 1  # odd H
     rc = lib.hvk_bias_gelu_fwd(ctypes.c_void_p(16), None, ctypes.c_void_p(16), 4, 12, None)
     assert rc == 2  # N % 8
+
+
+def test_library_options_table():
+    """libhvk reads no environment variable: its selectable forms are named options with a
+    range, set and read through the C ABI (include/hvk.h); unknown names and out-of-range
+    values are refused."""
+    from hvamd import _lib
+    defaults = {"wmsa_fwd_form": 0, "wmsa_bwd_nt": 0, "wmsa_bwd_slice_bytes": 1 << 31,
+                "gemm_pp": 0, "tile_wide": -1, "dw_tile": 5}
+    for name, v in defaults.items():
+        assert _lib.get_option(name) == v, name
+    with _lib.option("wmsa_fwd_form", 1):
+        assert _lib.get_option("wmsa_fwd_form") == 1
+    assert _lib.get_option("wmsa_fwd_form") == 0
+    for name, bad in [("wmsa_fwd_form", 2), ("dw_tile", 3), ("no_such_option", 0)]:
+        with pytest.raises(RuntimeError):
+            _lib.set_option(name, bad)
+    assert _lib.load().hvk_gemm_set_pp(0) == 0
+    src = os.path.join(ROOT, "hierarchical-vision_amd", "csrc")
+    for f in os.listdir(src):
+        if f.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(src, f)).read(), f
 
 
 def test_ops_refuse_cpu_tensors():
