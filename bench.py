@@ -12,7 +12,8 @@ exits with its status; under an external launcher WORLD_SIZE must equal --gpus.
 A step = forward + HXE loss + backward (bucketed RCCL all-reduce overlapped) + grad-norm
 clip + DecoupledSGDW update, bf16 autocast, f32 master weights; synthetic images/labels
 resident in HBM.  Rank 0 prints one JSON line.  The W-MSA roofline is measured live with
-HIP events around every W-MSA launch inside the timed steps; the CPU baseline (rank 0,
+dispatch-packet events around every W-MSA launch of extra steps right after the timed ones (the
+timed region carries no timer); the CPU baseline (rank 0,
 N = 1 only) times the oracle's f32 CPU restatement of the same model + loss on a bounded
 sample.
 """
@@ -57,6 +58,8 @@ def parse():
                          "multi-rank flow with several ranks sharing one GPU")
     ap.add_argument("--roofline-steps", type=int, default=4,
                     help="graph mode: eager warm-up steps whose W-MSA launches are timed")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a libhvk option (include/hvk.h hvk_set_option) before the run; A/B runs")
     return ap.parse_args()
 
 
@@ -301,6 +304,10 @@ def main():
         if dist.get_world_size() != world:
             raise RuntimeError(f"RCCL sees {dist.get_world_size()} ranks, expected {world}")
     import hvamd.ops as ops
+    from hvamd import _lib
+    for o in args.opt:
+        name, _, val = o.partition("=")
+        _lib.set_option(name, int(val))
 
     cfg, tax, model, trainer = build(args, device)
     img = model.module.patch_embed.img_size[0]
@@ -333,11 +340,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if timing and not args.graph:
-        # W-MSA launches timed by their own dispatch packets over the timed steps; the GEMMs'
-        # ~250 launches per step would perturb `value` (4 % measured), so their timer runs
-        # over extra steps after the timed region
-        ops.kernel_timer_start(kinds=ops.TIMER_WMSA)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -347,6 +349,14 @@ def main():
     elapsed = time.perf_counter() - t0
     gemm_timer, gemm_steps = None, 0
     if timing and not args.graph:
+        # the kernel timers run over extra steps after the timed region, so `value` is a clean
+        # wall time: W-MSA launches timed by their own dispatch packets, then the GEMMs (their
+        # ~250 launches per step perturb the step by ~4 %)
+        timed_steps = min(args.steps, 10)
+        ops.kernel_timer_start(kinds=ops.TIMER_WMSA)
+        for _ in range(timed_steps):
+            step()
+        torch.cuda.synchronize()
         launches = {k: ops.kernel_timer_launches(k) for k in (0, 1)}
         timer = ops.kernel_timer_stop()
         gemm_steps = min(args.steps, 5)
@@ -407,7 +417,8 @@ def main():
         r["timing"] = ("dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps just "
                        "before the graph capture (replays carry no per-kernel events)" % timed_steps
                        if args.graph else
-                       "dispatch-packet events (hipExtLaunchKernelGGL) over the timed steps")
+                       "dispatch-packet events (hipExtLaunchKernelGGL) over %d eager steps after the "
+                       "timed region" % timed_steps)
         if traffic is not None:
             r["algorithmic_bytes_per_launch"] = work["fwd_bytes"] // n_launch
             r["traffic_source"] = TRAFFIC_SOURCE

@@ -14,6 +14,7 @@
 //    (as gemm.hip), so a lane ends with 8 consecutive output columns of one row: 16-B stores.
 #include <stdlib.h>
 
+#include "gemm_xr.h"
 #include "hvk_common.h"
 
 // experiment builds (tools/probe/Makefile, NOT the product): 1 no MFMA, 2 no stores, 3 no DMA,
@@ -577,6 +578,10 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
   {
     const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
+    if (r >= 0) return r;
+  }
+  if (hvk_opt(HVK_OPT_GEMM_XR)) {  // the persistent row-range kernel where it has a plan
+    const int r = hvk_xr::launch(EPI, X, W, bias, Y, Y2, M, N, K, st);
     if (r >= 0) return r;
   }
   // the fused fc1 + GELU epilogue (EPI 1) at K >= 384 (stages 2-3) prefers 128-column tiles:

@@ -179,6 +179,61 @@ def test_gemm_tile_widths_bit_identical(M, K, N):
     assert torch.equal(out[0].view(torch.int16), out[1].view(torch.int16))
 
 
+@pytest.mark.parametrize("M,K,N,epi", [(50176, 384, 1152, 0), (50176, 1536, 384, 0), (50171, 384, 384, 0),
+                                       (12544, 768, 2304, 0), (12544, 3072, 768, 0), (12544, 2304, 768, 0),
+                                       (50176, 384, 1536, 1), (12544, 768, 3072, 1), (12540, 768, 3072, 1)])
+def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi):
+    """The persistent row-range kernel (gemm_xr.hip, option gemm_xr) accumulates every output in
+    the tile kernel's k order (64-deep steps, two 32-deep MFMAs each) and adds the bias the same
+    way: outputs bit-identical to gemm_nt_kernel's, on a ragged M too (rows past M dropped), for
+    the plain and the fc1 + GELU epilogue; and both within 1e-2 of an fp32 matmul."""
+    from hvamd import _lib
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * K + N + epi)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    out = {}
+    for mode in (0, 1):
+        y = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        y2 = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        with _lib.option("gemm_xr", mode):
+            if epi:
+                _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2),
+                          M, K, N, _lib.stream())
+            else:
+                _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), M, K, N, _lib.stream())
+            torch.cuda.synchronize()
+        out[mode] = (y, y2)
+    for i in range(2 if epi else 1):
+        a0, a1 = out[0][i], out[1][i]
+        assert torch.isnan(a1[M:].float()).all()  # nothing written past M
+        assert torch.equal(a0[:M].view(torch.int16), a1[:M].view(torch.int16)), i
+    ref = x.float() @ w.float().t() + b
+    rel = ((out[1][0][:M].float() - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("M,K,N", [(50176, 384, 1536), (12544, 768, 3072), (50170, 384, 1536)])
+def test_gemm_xr_gelu_bwd_bit_identical_to_tile_kernel(M, K, N):
+    """fc2's input gradient through GELU' (hvk_gemm_gelu_bwd) on the persistent row-range
+    kernel: bit-identical to the tile kernel (same k order, same GELU' of the same h)."""
+    from hvamd import _lib
+    g = torch.Generator(device="cuda").manual_seed(M + K + 5 * N)
+    gy = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    out = {}
+    for mode in (0, 1):
+        gh = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        with _lib.option("gemm_xr", mode):
+            _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(gy), _lib.ptr(w), _lib.ptr(h), _lib.ptr(gh), M, K, N, _lib.stream())
+            torch.cuda.synchronize()
+        out[mode] = gh
+    assert torch.isnan(out[1][M:].float()).all()
+    assert torch.equal(out[0][:M].view(torch.int16), out[1][:M].view(torch.int16))
+
+
 @pytest.mark.parametrize("N", [384, 256, 192])
 def test_gemm_tile_sparse_pattern_pins_layout(N):
     """One nonzero token row and one nonzero weight row: the output must be exactly one
