@@ -37,7 +37,7 @@ OptDef g_opts[HVK_OPT_COUNT] = {
     {"gemm_pp", 0, 0, 3},
     {"tile_wide", -1, -1, 1},
     {"dw_tile", 5, 4, 8},
-    {"gemm_xr", 0, 0, 1},
+    {"gemm_xr", 0, 0, 2},
 };
 int find_opt(const char* name) {
   if (!name) return -1;

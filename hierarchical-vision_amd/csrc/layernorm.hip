@@ -11,8 +11,12 @@
 // The backward also column-sums the branch gradient, which IS the folded bias's gradient,
 // so no separate bias-reduction pass exists.
 //
-// Layout: a row of C channels is owned by TPR lanes (power of two) holding EPT contiguous
-// channels each (16/32-byte bf16 loads, 32/64-byte f32 loads); a wave works on 64/TPR
+// Layout: a row of C channels is owned by TPR lanes (power of two); lane t holds EPT channels
+// as groups of 4 at channel 4 (i TPR + t), i < EPT / 4, so every wave-instruction reads or writes
+// whole lines: lanes t, t+1, ... cover adjacent 16-B f32 (8-B bf16) pieces of the row.  (The
+// round-1..3 layout gave a lane 8 contiguous channels: its two float4 accesses then sat 32 B
+// apart, each f32 instruction touching every line it read or wrote by halves -- 1.8x slower
+// at stage 0, tools/probe/ln_probe.hip, profiles/round4/ln_probe.txt.)  A wave works on 64/TPR
 // rows at once, grid-strided.  Row statistics are TPR-lane xor-shuffle reductions.
 #include "hvk_common.h"
 
@@ -20,51 +24,35 @@ namespace {
 
 constexpr int kWaves = 4;
 
+// group i of lane t: channels 4 (i TPR + t) .. +3
+template <int TPR>
+__device__ __forceinline__ int grp_c(int t, int i) { return 4 * (i * TPR + t); }
 // HVK_NT_SAVED bit 4: the LayerNorm kernels' streamed inputs (the GEMM output a, the f32
 // residual stream / its gradient, the bf16 gradient) are read for the last time in the pass
 // (a again only by the backward), so they are loaded nontemporally
-template <int EPT>
-__device__ __forceinline__ void load_bf16(const hvk_bf16* p, float v[EPT]) {
-#pragma unroll
-  for (int i = 0; i < EPT / 8; ++i) {
-    const uint4 w = (HVK_NT_SAVED & 16) ? hvk_ld16_nt(p + 8 * i) : reinterpret_cast<const uint4*>(p)[i];
-    float f[8];
-    hvk_unpack8(w, f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[8 * i + j] = f[j];
+__device__ __forceinline__ void ld4_bf16(const hvk_bf16* p, float* v) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = hvk_lo(u.x); v[1] = hvk_hi(u.x); v[2] = hvk_lo(u.y); v[3] = hvk_hi(u.y);
+}
+__device__ __forceinline__ void st4_bf16(hvk_bf16* p, const float* v) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
+}
+__device__ __forceinline__ void ld4_f32(const float* p, float* v) {
+  const float4 w = *reinterpret_cast<const float4*>(p);
+  v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+}
+__device__ __forceinline__ void ld4_f32_stream(const float* p, float* v) {
+  if (HVK_NT_SAVED & 16) {
+    const uint4 u = hvk_ld16_nt(p);
+    v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y); v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
+  } else {
+    ld4_f32(p, v);
   }
 }
-template <int EPT>
-__device__ __forceinline__ void store_bf16(hvk_bf16* p, const float v[EPT]) {
-#pragma unroll
-  for (int i = 0; i < EPT / 8; ++i) reinterpret_cast<uint4*>(p)[i] = hvk_pack8(v + 8 * i);
-}
-template <int EPT>
-__device__ __forceinline__ void load_f32(const float* p, float v[EPT]) {
-#pragma unroll
-  for (int i = 0; i < EPT / 4; ++i) {
-    const float4 w = reinterpret_cast<const float4*>(p)[i];
-    v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
-  }
-}
-template <int EPT>
-__device__ __forceinline__ void load_f32_stream(const float* p, float v[EPT]) {
-  if (!(HVK_NT_SAVED & 16)) {
-    load_f32<EPT>(p, v);
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < EPT / 4; ++i) {
-    const uint4 u = hvk_ld16_nt(p + 4 * i);
-    const float4 w = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
-    v[4 * i] = w.x; v[4 * i + 1] = w.y; v[4 * i + 2] = w.z; v[4 * i + 3] = w.w;
-  }
-}
-template <int EPT>
-__device__ __forceinline__ void store_f32(float* p, const float v[EPT]) {
-#pragma unroll
-  for (int i = 0; i < EPT / 4; ++i)
-    reinterpret_cast<float4*>(p)[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+__device__ __forceinline__ void st4_f32(float* p, const float* v, bool nt) {
+  const uint4 u = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3]));
+  if (nt) hvk_st16_nt(p, u);
+  else *reinterpret_cast<uint4*>(p) = u;
 }
 template <int TPR>
 __device__ __forceinline__ float group_sum(float v) {
@@ -81,61 +69,62 @@ struct LnFwd {
 
 template <int EPT, int TPR>
 __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
-  constexpr int RPW = 64 / TPR;
+  constexpr int RPW = 64 / TPR, NG = EPT / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane / TPR, t = lane % TPR;
-  const int c0 = t * EPT;
-  const bool act = c0 < p.C;
   float gm[EPT], bt[EPT], ab[EPT];
+  bool ok[NG];
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) { gm[j] = 0.f; bt[j] = 0.f; ab[j] = 0.f; }
-  if (act) {
-    load_f32<EPT>(p.gamma + c0, gm);
-    load_f32<EPT>(p.beta + c0, bt);
-    if (p.abias) load_f32<EPT>(p.abias + c0, ab);
+  for (int i = 0; i < NG; ++i) {
+    const int c = grp_c<TPR>(t, i);
+    ok[i] = c < p.C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gm[4 * i + j] = bt[4 * i + j] = ab[4 * i + j] = 0.f;
+    if (ok[i]) {
+      ld4_f32(p.gamma + c, gm + 4 * i);
+      ld4_f32(p.beta + c, bt + 4 * i);
+      if (p.abias) ld4_f32(p.abias + c, ab + 4 * i);
+    }
   }
   const float invC = 1.f / p.C;
   for (int row = (blockIdx.x * kWaves + wave) * RPW + sub; row < p.rows;
        row += gridDim.x * kWaves * RPW) {
+    const size_t rb = (size_t)row * p.C;
     float v[EPT];
     float s = 0.f;
-    if (act) {
-      load_bf16<EPT>(p.a + (size_t)row * p.C + c0, v);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) { v[j] += ab[j]; s += v[j]; }
-    } else {
+    for (int i = 0; i < NG; ++i) {
+      if (ok[i]) {
+        ld4_bf16(p.a + rb + grp_c<TPR>(t, i), v + 4 * i);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) v[j] = 0.f;
+        for (int j = 0; j < 4; ++j) { v[4 * i + j] += ab[4 * i + j]; s += v[4 * i + j]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
+      }
     }
     const float mu = group_sum<TPR>(s) * invC;
     float ss = 0.f;
-    if (act) {
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) { const float d = v[j] - mu; ss += d * d; }
-    }
+    for (int i = 0; i < NG; ++i)
+      if (ok[i]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[4 * i + j] - mu; ss += d * d; }
+      }
     const float rs = rsqrtf(group_sum<TPR>(ss) * invC + p.eps);
-    if (act) {
-      const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-      float r[EPT];
-      if (p.x0) load_f32_stream<EPT>(p.x0 + (size_t)row * p.C + c0, r);
-      else {
+    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) r[j] = 0.f;
-      }
+    for (int i = 0; i < NG; ++i) {
+      if (!ok[i]) continue;
+      const int c = grp_c<TPR>(t, i);
+      float r[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.x0) ld4_f32_stream(p.x0 + rb + c, r);
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) r[j] += ((v[j] - mu) * rs * gm[j] + bt[j]) * sc;
-      if (HVK_NT_SAVED & 2) {  // the f32 stream is read again only at the next LayerNorm
-#pragma unroll
-        for (int i = 0; i < EPT / 4; ++i)
-          hvk_st16_nt(p.x + (size_t)row * p.C + c0 + 4 * i,
-                      make_uint4(__float_as_uint(r[4 * i]), __float_as_uint(r[4 * i + 1]),
-                                 __float_as_uint(r[4 * i + 2]), __float_as_uint(r[4 * i + 3])));
-      } else {
-        store_f32<EPT>(p.x + (size_t)row * p.C + c0, r);
-      }
-      if (p.xb) store_bf16<EPT>(p.xb + (size_t)row * p.C + c0, r);
-      if (t == 0) { p.mean[row] = mu; p.rstd[row] = rs; }
+      for (int j = 0; j < 4; ++j) r[j] += ((v[4 * i + j] - mu) * rs * gm[4 * i + j] + bt[4 * i + j]) * sc;
+      st4_f32(p.x + rb + c, r, HVK_NT_SAVED & 2);  // the f32 stream is read again only at the next LayerNorm
+      if (p.xb) st4_bf16(p.xb + rb + c, r);
     }
+    if (t == 0) { p.mean[row] = mu; p.rstd[row] = rs; }
   }
 }
 
@@ -150,12 +139,10 @@ struct LnBwd {
 
 template <int EPT, int TPR>
 __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
-  constexpr int RPW = 64 / TPR;
+  constexpr int RPW = 64 / TPR, NG = EPT / 4;
   __shared__ float red[kWaves][3][TPR * EPT];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int sub = lane / TPR, t = lane % TPR;
-  const int c0 = t * EPT;
-  const bool act = c0 < p.C;
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < p.C; i += blockDim.x) {
       p.zero0[i] = 0.f;
@@ -163,67 +150,72 @@ __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
       if (p.zero2) p.zero2[i] = 0.f;
     }
   float gm[EPT], ab[EPT], dg[EPT], db[EPT], dab[EPT];
+  bool ok[NG];
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) { gm[j] = ab[j] = dg[j] = db[j] = dab[j] = 0.f; }
-  if (act) {
-    load_f32<EPT>(p.gamma + c0, gm);
-    if (p.abias) load_f32<EPT>(p.abias + c0, ab);
+  for (int i = 0; i < NG; ++i) {
+    const int c = grp_c<TPR>(t, i);
+    ok[i] = c < p.C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gm[4 * i + j] = ab[4 * i + j] = dg[4 * i + j] = db[4 * i + j] = dab[4 * i + j] = 0.f;
+    if (ok[i]) {
+      ld4_f32(p.gamma + c, gm + 4 * i);
+      if (p.abias) ld4_f32(p.abias + c, ab + 4 * i);
+    }
   }
   const float invC = 1.f / p.C;
   for (int row = (blockIdx.x * kWaves + wave) * RPW + sub; row < p.rows;
        row += gridDim.x * kWaves * RPW) {
+    const size_t rb = (size_t)row * p.C;
     float y[EPT], go[EPT], gy[EPT];
     float s1 = 0.f, s2 = 0.f;
     const float mu = p.mean[row], rs = p.rstd[row];
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-    if (act) {
-      load_bf16<EPT>(p.a + (size_t)row * p.C + c0, y);
-      if (p.gx) load_f32_stream<EPT>(p.gx + (size_t)row * p.C + c0, go);
-      else {
 #pragma unroll
-        for (int j = 0; j < EPT; ++j) go[j] = 0.f;
+    for (int i = 0; i < NG; ++i) {
+      float* yi = y + 4 * i;
+      float* gi = go + 4 * i;
+      if (ok[i]) {
+        const int c = grp_c<TPR>(t, i);
+        ld4_bf16(p.a + rb + c, yi);
+        if (p.gx) ld4_f32_stream(p.gx + rb + c, gi);
+        else gi[0] = gi[1] = gi[2] = gi[3] = 0.f;
+        if (p.gxb) {
+          float q[4];
+          ld4_bf16(p.gxb + rb + c, q);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gi[j] += q[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int e = 4 * i + j;
+          y[e] = (y[e] + ab[e] - mu) * rs;
+          const float o = go[e] * sc;  // gradient of the LN output
+          dg[e] += o * y[e];
+          db[e] += o;
+          gy[e] = o * gm[e];
+          s1 += gy[e];
+          s2 += gy[e] * y[e];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) yi[j] = gi[j] = gy[4 * i + j] = 0.f;
       }
-      if (p.gxb) {
-        float q[EPT];
-        load_bf16<EPT>(p.gxb + (size_t)row * p.C + c0, q);
-#pragma unroll
-        for (int j = 0; j < EPT; ++j) go[j] += q[j];
-      }
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        y[j] = (y[j] + ab[j] - mu) * rs;
-        const float o = go[j] * sc;  // gradient of the LN output
-        dg[j] += o * y[j];
-        db[j] += o;
-        gy[j] = o * gm[j];
-        s1 += gy[j];
-        s2 += gy[j] * y[j];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < EPT; ++j) y[j] = go[j] = gy[j] = 0.f;
     }
     s1 = group_sum<TPR>(s1) * invC;
     s2 = group_sum<TPR>(s2) * invC;
-    if (act) {
-      float d[EPT];
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) {
-        d[j] = rs * (gy[j] - s1 - y[j] * s2);
-        dab[j] += d[j];
-      }
-      store_bf16<EPT>(p.ga + (size_t)row * p.C + c0, d);
-      if (p.gx0) {
-        if (HVK_NT_SAVED & 4) {
+    for (int i = 0; i < NG; ++i) {
+      if (!ok[i]) continue;
+      const int c = grp_c<TPR>(t, i);
+      float d[4];
 #pragma unroll
-          for (int i = 0; i < EPT / 4; ++i)
-            hvk_st16_nt(p.gx0 + (size_t)row * p.C + c0 + 4 * i,
-                        make_uint4(__float_as_uint(go[4 * i]), __float_as_uint(go[4 * i + 1]),
-                                   __float_as_uint(go[4 * i + 2]), __float_as_uint(go[4 * i + 3])));
-        } else {
-          store_f32<EPT>(p.gx0 + (size_t)row * p.C + c0, go);
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int e = 4 * i + j;
+        d[j] = rs * (gy[e] - s1 - y[e] * s2);
+        dab[e] += d[j];
       }
+      st4_bf16(p.ga + rb + c, d);
+      if (p.gx0) st4_f32(p.gx0 + rb + c, go + 4 * i, HVK_NT_SAVED & 4);
     }
   }
   // fold the RPW row slots of the wave (lanes t, t+TPR, ...), then the waves via LDS
@@ -238,9 +230,10 @@ __global__ __launch_bounds__(64 * kWaves) void ln_bwd_kernel(LnBwd p) {
   if (sub == 0) {
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
-      red[wave][0][c0 + j] = dg[j];
-      red[wave][1][c0 + j] = db[j];
-      red[wave][2][c0 + j] = dab[j];
+      const int c = grp_c<TPR>(t, j / 4) + (j & 3);  // < TPR * EPT
+      red[wave][0][c] = dg[j];
+      red[wave][1][c] = db[j];
+      red[wave][2][c] = dab[j];
     }
   }
   __syncthreads();
@@ -273,7 +266,8 @@ __global__ __launch_bounds__(64) void colsum_kernel(const float* part, int nblk,
 
 constexpr int kBwdBlocks = 1024;
 
-// (EPT, TPR) for a channel count: TPR * EPT >= C, TPR a power of two <= 64
+// (EPT, TPR) for a channel count: TPR * EPT >= C, TPR a power of two <= 64 (tools/probe/
+// ln_probe.hip: 8 channels per lane up to C = 512, the fastest at C = 96 / 192 / 384, 16 above)
 int pick_layout(int C, int& ept, int& tpr) {
   if (C % 8) return 1;
   ept = C > 512 ? 16 : 8;

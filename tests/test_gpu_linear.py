@@ -182,7 +182,8 @@ def test_gemm_tile_widths_bit_identical(M, K, N):
 @pytest.mark.parametrize("M,K,N,epi", [(50176, 384, 1152, 0), (50176, 1536, 384, 0), (50171, 384, 384, 0),
                                        (12544, 768, 2304, 0), (12544, 3072, 768, 0), (12544, 2304, 768, 0),
                                        (50176, 384, 1536, 1), (12544, 768, 3072, 1), (12540, 768, 3072, 1)])
-def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi):
+@pytest.mark.parametrize("xr", [1, 2])
+def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi, xr):
     """The persistent row-range kernel (gemm_xr.hip, option gemm_xr) accumulates every output in
     the tile kernel's k order (64-deep steps, two 32-deep MFMAs each) and adds the bias the same
     way: outputs bit-identical to gemm_nt_kernel's, on a ragged M too (rows past M dropped), for
@@ -197,7 +198,7 @@ def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi):
     for mode in (0, 1):
         y = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
         y2 = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        with _lib.option("gemm_xr", mode):
+        with _lib.option("gemm_xr", xr if mode else 0):
             if epi:
                 _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2),
                           M, K, N, _lib.stream())
@@ -215,7 +216,8 @@ def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi):
 
 
 @pytest.mark.parametrize("M,K,N", [(50176, 384, 1536), (12544, 768, 3072), (50170, 384, 1536)])
-def test_gemm_xr_gelu_bwd_bit_identical_to_tile_kernel(M, K, N):
+@pytest.mark.parametrize("xr", [1, 2])
+def test_gemm_xr_gelu_bwd_bit_identical_to_tile_kernel(M, K, N, xr):
     """fc2's input gradient through GELU' (hvk_gemm_gelu_bwd) on the persistent row-range
     kernel: bit-identical to the tile kernel (same k order, same GELU' of the same h)."""
     from hvamd import _lib
@@ -226,7 +228,7 @@ def test_gemm_xr_gelu_bwd_bit_identical_to_tile_kernel(M, K, N):
     out = {}
     for mode in (0, 1):
         gh = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        with _lib.option("gemm_xr", mode):
+        with _lib.option("gemm_xr", xr if mode else 0):
             _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(gy), _lib.ptr(w), _lib.ptr(h), _lib.ptr(gh), M, K, N, _lib.stream())
             torch.cuda.synchronize()
         out[mode] = gh
