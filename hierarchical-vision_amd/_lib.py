@@ -33,12 +33,19 @@ SIGNATURES = {
     "hvk_get_option": (_i, [ctypes.c_char_p, _p]),
     "hvk_wmsa_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_workspace_bytes": (_sz, [_i, _i]),
+    "hvk_wmsa_fwd_normed": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
+    "hvk_wmsa_bwd_normed": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i,
+                                 _p]),
+    "hvk_qk_normalize": (_i, [_p, _p, _i, _i, _p]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
     "hvk_linear_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_cpb_fwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p]),
     "hvk_cpb_bwd_workspace_bytes": (_sz, [_i, _i]),
     "hvk_cpb_bwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
                          _p]),
+    "hvk_linear_qkv_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_gemm_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_supported": (_i, [_i, _i, _i]),
@@ -47,6 +54,10 @@ SIGNATURES = {
     "hvk_gemm_gelu_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_set_pp": (_i, [_i]),
     "hvk_weight_grad_supported": (_i, [_i, _i, _i]),
+    "hvk_head_supported": (_i, [_i, _i, _i]),
+    "hvk_head_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_head_bwd_workspace_bytes": (_sz, [_i, _i, _i]),
+    "hvk_head_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_cast_weights": (_i, [_i, _p, _p, _p, _p, _p, _p]),
     "hvk_block_bias_fwd": (_i, [_p, _p, _p, _p, _i, _p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p,
                                 _p]),
@@ -93,7 +104,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 8  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
+ABI_VERSION = 9  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
 
 
 def load():

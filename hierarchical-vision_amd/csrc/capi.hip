@@ -21,7 +21,7 @@ int hvk_set_error(int code, const char* fmt, ...) {
 
 const char* hvk_last_error_string(void) { return g_hvk_err; }
 
-int hvk_abi_version(void) { return 8; }
+int hvk_abi_version(void) { return 9; }
 
 }  // extern "C"
 

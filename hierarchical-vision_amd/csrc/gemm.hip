@@ -49,6 +49,9 @@ __device__ __forceinline__ int perm_row(int p) {
 // read from Y2 (the saved fc1 pre-activation), and csum[n] += sum over rows of gh (the fc1
 // bias gradient): per-lane register sums over the workgroup's row tiles, one 16-lane
 // shuffle reduction and one atomic per column and wave at the end.
+// EPI 4 (the qkv Linear of a w <= 8 W-MSA block): EPI 0 with every q and k head slice (columns
+// < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
+// 1 / max(||x||, eps) stored to rn [M, 2N/96] (passed in csum).
 template <int K, int BN, int WAVES, bool PREF, bool BIAS, int EPI = 0>
 __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __restrict__ X,
                                                           const hvk_bf16* __restrict__ W,
@@ -151,6 +154,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
       const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N * 2);
       const auto ry2 = hvk_tile_rsrc(Y2, 16 * tile, M, N * 2);
       const uint32_t yo = (uint32_t)(li * N + n0 + 8 * g) * 2;
+      float rq[EPI == 4 ? G::NT / 2 : 1];  // EPI 4: the row's 1/||x|| per head slice
+#pragma unroll
+      for (int j = 0; j < (EPI == 4 ? G::NT / 2 : 1); ++j) rq[j] = 0.f;
 #pragma unroll
       for (int j = 0; j < G::NT / 2; ++j) {
         float v[8];
@@ -182,7 +188,15 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
           v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
         }
-        const uint4 hv = hvk_pack8(v);
+        uint4 hv = hvk_pack8(v);
+        if constexpr (EPI == 4) {
+          const int qk_cols = 2 * (N / 3), col = n0 + 32 * j;
+          if (col < qk_cols) {  // wave-uniform: the v column blocks skip it
+            float r;
+            hv = hvk_head_normalize8(hv, r);  // all 64 lanes take part in the group sums
+            rq[j] = r;
+          }
+        }
         if (EPI == 1 && (HVK_NT_SAVED & 1))
           hvk_bst16_nt(ry, yo + 64 * j, hv);
         else
@@ -197,6 +211,22 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             u[e + 1] = y.y;
           }
           hvk_bst16(ry2, yo + 64 * j, hvk_pack8(u));
+        }
+      }
+      if constexpr (EPI == 4) {
+        // the row's 1/||x|| per q / k head slice j (all 4 lanes of a row hold every one): lane g
+        // stores slices g, g + 4, ..., a buffer store dropped past M and past the q / k columns
+        const int hc = 2 * (N / 3) / 32, row = 16 * tile + li;
+        const int nqk = (2 * (N / 3) - n0) / 32;  // q / k slices of this column block (prefix)
+        const auto rr = hvk_rsrc(csum, (size_t)M * hc * 4);
+#pragma unroll
+        for (int j0 = 0; j0 < G::NT / 2; j0 += 4) {
+          float r = rq[j0];
+#pragma unroll
+          for (int k = 1; k < 4; ++k)
+            if (j0 + k < G::NT / 2) r = g == k ? rq[j0 + k] : r;
+          const int j = j0 + g;
+          hvk_bst4f(rr, row < M && j < nqk && j < G::NT / 2 ? (uint32_t)(row * hc + n0 / 32 + j) * 4 : HVK_OOB, r);
         }
       }
     }
@@ -568,6 +598,28 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
 #undef HVK_LIN3
 #undef HVK_LIN
   return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_fwd: config K=%d BN=%d not built", K, c->BN);
+}
+
+int hvk_linear_qkv_supported(int M, int K, int N) {
+  const LinCfg* c = pick(K, N);
+  return M > 0 && c && N == 3 * K && K % 32 == 0 &&
+         ((K == 96 && c->BN == 288) || (K == 192 && c->BN == 288) || (K == 128 && c->BN == 192) ||
+          (K == 256 && c->BN == 128)) && c->waves == 8 && c->pref == 1;
+}
+
+int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K, int N,
+                       void* stream) {
+  if (!x || !w || !y || !rn) return hvk_set_error(HVK_EINVAL, "hvk_linear_qkv_fwd: null pointer");
+  if (!hvk_linear_qkv_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_qkv_fwd: shape M=%d K=%d N=%d not built", M, K, N);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
+  const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
+  hvk_bf16* Y = static_cast<hvk_bf16*>(y);
+  if (K == 96) return launch_linear<96, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
+  if (K == 192) return launch_linear<192, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
+  if (K == 128) return launch_linear<128, 192, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
+  return launch_linear<256, 128, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
 }
 
 int hvk_linear_gelu_supported(int M, int K, int N) {

@@ -93,11 +93,14 @@ __device__ __forceinline__ void load_h_tile(uint4 (&hp)[EPI == 2 ? HM : 1][NT / 
   }
 }
 
+// EPI 4 (the qkv Linear of a w <= 8 W-MSA block): Y = acc + bias with every q and k head slice
+// (columns < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
+// 1 / max(||x||, eps) stored to rn [M, 2N/96]; the v columns as EPI 0.
 template <int EPI, int NT, int MT, int HPRE = 0>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
                                               int N, int row0, int col0,
-                                              const uint4 (*hpre)[NT / 2] = nullptr) {
+                                              const uint4 (*hpre)[NT / 2] = nullptr, float* __restrict__ rn = nullptr) {
   // HPRE: h of token tiles 0 .. HPRE-1 was loaded early by the caller (hpre)
   const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   float bv[NT / 2][8];
@@ -119,6 +122,8 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
     load_h_tile<EPI, NT, MT, HPRE, MT>(hp, Y2, M, N, row0, col0);
   }
   hvk_u32x4 pk[MT][NT / 2], pg[EPI == 1 ? MT : 1][NT / 2];
+  float rv[EPI == 4 ? MT : 1][NT / 2];
+  const int qk_cols = 2 * (N / 3);
 #pragma unroll
   for (int b = 0; b < MT; ++b)
 #pragma unroll
@@ -146,6 +151,14 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
       const uint4 hv = hvk_pack8(v);
       pk[b][j] = __builtin_bit_cast(hvk_u32x4, hv);
       if (EPI == 1) pg[b][j] = __builtin_bit_cast(hvk_u32x4, hvk_gelu8_bf16(hv));  // GELU of the rounded h
+      if constexpr (EPI == 4) {
+        rv[b][j] = 0.f;
+        if (col0 + 32 * j < qk_cols) {  // wave-uniform: the v column blocks skip it
+          float r;
+          pk[b][j] = __builtin_bit_cast(hvk_u32x4, hvk_head_normalize8(hv, r));  // all 64 lanes
+          rv[b][j] = r;
+        }
+      }
     }
   // pin the packing here (else hipcc sinks it into each row's store branch and reuses the
   // registers of the previous row's stores)
@@ -169,6 +182,15 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
         *reinterpret_cast<hvk_u32x4*>(Y + o) = pk[b][j];
       if (EPI == 1) *reinterpret_cast<hvk_u32x4*>(Y2 + o) = pg[b][j];
     }
+    if constexpr (EPI == 4) {
+      // the row's 1/||x|| of head slices j = 0 .. NT/2-1 (every lane of the row holds all of them):
+      // lane gq stores slice gq, one store instruction per row instead of one per slice
+      float r = rv[b][0];
+#pragma unroll
+      for (int j = 1; j < NT / 2; ++j) r = gq == j ? rv[b][j] : r;
+      const int c = col0 + 32 * gq;
+      if (gq < NT / 2 && c < qk_cols) rn[(size_t)row * (qk_cols / 32) + c / 32] = r;
+    }
   }
 }
 
@@ -178,7 +200,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
                                                         const float* __restrict__ bias,
                                                         hvk_bf16* __restrict__ Y,
                                                         hvk_bf16* __restrict__ Y2, int M, int N,
-                                                        int K, int mtiles) {
+                                                        int K, int mtiles, float* __restrict__ rn) {
   using T = TileCfg<TN>;
   constexpr int BN = T::BN, STAGE_BYTES = T::STAGE, TILE_BYTES = T::WTILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -320,7 +342,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre);
+  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
@@ -551,7 +573,7 @@ int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16*
 
 template <int EPI, bool PIPE, int TN>
 int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                 int M, int N, int K, hipStream_t st) {
+                 int M, int N, int K, hipStream_t st, float* rn = nullptr) {
   using T = TileCfg<TN>;
   static bool attr = false;
   if (!attr) {
@@ -563,7 +585,7 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / T::BN));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
-                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles);
+                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }
@@ -571,11 +593,16 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
 // 128 x 128 or 128 x 192 tiles
 template <int EPI>
 int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                int M, int N, int K, hipStream_t st) {
+                int M, int N, int K, hipStream_t st, float* rn = nullptr) {
   // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1536 case
   // (tools/bench_gemm.py, interleaved: 3-25 % faster on the stage-2/3 shapes, 6 % slower on
   // the stage-2 projection); option "tile_wide" 0 / 1 forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
+  if constexpr (EPI == 4) {  // the qkv form: the 128-row tile kernel only
+    if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536)))
+      return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn);
+    return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn);
+  } else {
   {
     const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
     if (r >= 0) return r;
@@ -593,6 +620,7 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   if (N % TileCfg<4>::BN == 0 && !wide)
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st);
   return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st);
+  }
 }
 
 }  // namespace
@@ -636,6 +664,15 @@ int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, in
                         static_cast<hvk_bf16*>(gh),
                         const_cast<hvk_bf16*>(static_cast<const hvk_bf16*>(h)), M, N, K,
                         static_cast<hipStream_t>(stream));
+}
+
+int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
+                     int N, void* stream) {
+  if (!x || !w || !y || !rn) return hvk_set_error(HVK_EINVAL, "hvk_gemm_qkv_fwd: null pointer");
+  if (!hvk_gemm_supported(M, K, N) || N % 96)
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_qkv_fwd: M=%d K=%d N=%d (N = 3C, 32 | C)", M, K, N);
+  return launch_tile<4>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
+                        static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream), rn);
 }
 
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M, int K,

@@ -181,6 +181,12 @@ __device__ __forceinline__ void hvk_bst16(__amdgpu_buffer_rsrc_t r, uint32_t off
 __device__ __forceinline__ void hvk_bst16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hvk_u32x4, v), r, off, 0, 2);  // nt
 }
+__device__ __forceinline__ void hvk_bst4f(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ float hvk_bld4f(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
 __device__ __forceinline__ uint4 hvk_bld16_nt(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
 }
@@ -356,6 +362,35 @@ __device__ __forceinline__ int hvk_pair_col(int gq) { return 16 * (gq & 1) + 8 *
 
 __device__ __forceinline__ float hvk_group4_sum(float v) { return hvk_xor32_sum(hvk_xor16_sum(v)); }
 __device__ __forceinline__ float hvk_group4_max(float v) { return hvk_xor32_max(hvk_xor16_max(v)); }
+
+// Head normalisation of the W-MSA q / k slices (F.normalize, swinv2.py:229) where the qkv rows
+// are produced (the GEMM epilogues, hvk_qk_normalize): a lane holds 8 consecutive channels of one
+// row and lanes l, l^16, l^32, l^48 the head's 32 channels; hv = the rounded bf16 qkv values.
+// Returns the normalised bf16 values and rn = 1 / max(||x||, 1e-12) -- the arithmetic of
+// wmsa_common.h's l2_normalize (dot2 sum of squares, group-4 sum, rsq), which the w <= 8
+// attention kernels ran on the loaded rows before round 4.
+__device__ __forceinline__ uint4 hvk_head_normalize8(uint4 v, float& rn) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  auto d2 = [](uint32_t w, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, w), __builtin_bit_cast(bf16x2_t, w), c, false);
+  };
+  float ss = d2(v.w, d2(v.z, d2(v.y, d2(v.x, 0.f))));
+  float f[8];
+  hvk_unpack8(v, f);
+  ss = hvk_group4_sum(ss);
+  rn = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= rn;
+  return hvk_pack8(f);
+}
+// 8 packed bf16 times a scalar, rounded back to bf16
+__device__ __forceinline__ uint4 hvk_scale8(uint4 v, float m) {
+  float f[8];
+  hvk_unpack8(v, f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= m;
+  return hvk_pack8(f);
+}
 
 // max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors)
 __device__ __forceinline__ float hvk_row16_max(float v) {

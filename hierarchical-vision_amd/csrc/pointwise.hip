@@ -104,7 +104,46 @@ constexpr int kBwdRowBlocks = 512;
 
 }  // namespace
 
+namespace {
+
+// q / k head normalisation of a qkv tensor in place (hvk_qk_normalize): a wave owns 16 rows x one
+// head (lane = row li, 8-channel chunk g), the layout of the fused GEMM epilogues, so the sums
+// of squares reduce in the same order and the results are bit-identical to theirs
+__global__ __launch_bounds__(256) void qk_normalize_kernel(hvk_bf16* __restrict__ qkv, float* __restrict__ rn,
+                                                           int T, int C) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int heads2 = 2 * C / 32;
+  const long long item = (long long)blockIdx.x * 4 + wave;  // (16-row tile, head)
+  const int hd = (int)(item % heads2);
+  const long long row = (item / heads2) * 16 + li;
+  if (item / heads2 * 16 >= T) return;
+  const bool ok = row < T;
+  const size_t off = (size_t)(ok ? row : 0) * 3 * C + hd * 32 + 8 * g;
+  uint4 v = *reinterpret_cast<const uint4*>(qkv + off);
+  float r;
+  v = hvk_head_normalize8(v, r);  // all 64 lanes take part in the group sums
+  if (ok) {
+    *reinterpret_cast<uint4*>(qkv + off) = v;
+    if (g == 0) rn[(size_t)row * heads2 + hd] = r;
+  }
+}
+
+}  // namespace
+
 extern "C" {
+
+int hvk_qk_normalize(void* qkv, float* rn, int T, int C, void* stream) {
+  if (!qkv || !rn) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: null pointer");
+  if (T <= 0 || C <= 0 || C % 32) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: T=%d C=%d (C %% 32)", T, C);
+  const long long items = (long long)((T + 15) / 16) * (2 * C / 32);
+  const long long grid = (items + 3) / 4;
+  if (grid > 0x7fffffffLL) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: too many rows");
+  hipLaunchKernelGGL(qk_normalize_kernel, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<hvk_bf16*>(qkv), rn, T, C);
+  HVK_CHECK_LAUNCH("hvk_qk_normalize");
+  return HVK_OK;
+}
 
 size_t hvk_bias_gelu_bwd_workspace_bytes(int N) {
   return (size_t)kBwdRowBlocks * N * sizeof(float);

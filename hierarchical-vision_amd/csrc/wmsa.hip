@@ -33,6 +33,9 @@ namespace {
 using namespace hvk_wmsa;
 
 constexpr int kWaves = 4;
+#ifndef HVK_BWD_PROBE  // tools/ timing probes of the w <= 8 backward (results wrong when set)
+#define HVK_BWD_PROBE 0
+#endif
 #ifndef HVK_BWD_PF  // 1: next window's inputs loaded under phase B (see wmsa_bwd_kernel)
 #define HVK_BWD_PF 1
 #endif
@@ -190,7 +193,7 @@ __device__ unsigned long long g_bwd_stamps[8];
   } while (0)
 #endif
 
-template <int WIN, bool QNT>
+template <int WIN, bool QNT, bool NORMED>
 __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   using K = WinCfg<WIN>;
   using PC = PairCfg<WIN>;
@@ -230,6 +233,10 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   const size_t T = (size_t)g.B * g.H * g.W;
   const auto r_qkv = hvk_rsrc(a.qkv, T * C3 * 2), r_dout = hvk_rsrc(a.dout, T * C * 2);
   const auto r_dqkv = hvk_rsrc(a.dqkv, T * C3 * 2);
+  // NORMED: q^, k^ and their 1/||x|| (a.rn) from the qkv GEMM's epilogue (a compile-time form:
+  // a runtime branch around the rn loads left the compiler's wait counts conservative)
+  constexpr bool normed = NORMED;
+  const auto r_rn = hvk_rsrc(a.rn, normed ? T * 2 * g.nH * 4 : 0);
   // LDS byte offsets as one per-lane base + compile-time immediates (tile t of a 16-row image
   // = +1024 B; 8-B unit 4dt + u = +512 dt B): few live address registers, no spills
   const char* const qsb = reinterpret_cast<const char*>(qs);
@@ -310,13 +317,23 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
     const bool edge_r = g.shift && wh == g.nWh - 1, edge_c = g.shift && ww == g.nWw - 1;
     int row[TPW];
     float rnq[TPW], rnk[TPW];
+    if constexpr (normed) {  // first used after phase A: issued here, ahead of the dK / dV stores below
+#pragma unroll
+      for (int j = 0; j < TPW; ++j) {
+        const uint32_t orn = rown[j] < 0 ? HVK_OOB : (uint32_t)(rown[j] * 2 * g.nH + h) * 4;
+        rnq[j] = hvk_bld4f(r_rn, orn);
+        rnk[j] = hvk_bld4f(r_rn, orn + 4 * g.nH);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       row[j] = rown[j];
       const int t = hf + 2 * j;
       if (act && t < NT) {
-        qf[j] = l2_normalize(qf[j], rnq[j]);
-        kf[j] = l2_normalize(kf[j], rnk[j]);
+        if constexpr (!normed) {
+          qf[j] = l2_normalize(qf[j], rnq[j]);
+          kf[j] = l2_normalize(kf[j], rnk[j]);
+        }
         const int o16 = o_row + 1024 * t;
         *reinterpret_cast<uint4*>((char*)qsb + o16) = qf[j];
         *reinterpret_cast<uint4*>((char*)ksb + o16) = kf[j];
@@ -556,8 +573,10 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   __syncthreads();
   const float* red0 = reinterpret_cast<const float*>(img0);
   float* dst = a.dbias_acc + (size_t)h * K::TAB;
+#if HVK_BWD_PROBE != 1  // timing probe: without the CPB-gradient atomics (results wrong)
   for (int e = threadIdx.x; e < K::TAB; e += kThreads)
     atomicAdd(dst + e, (red0[e] + red0[PC::PAIR_LDS / 2 + e]) * inv_scale);
+#endif
   dscale = hvk_wave_sum(dscale);
   if (lane == 0) atomicAdd(a.dscale_acc + h, dscale * inv_scale);
 #pragma unroll
@@ -576,11 +595,11 @@ __global__ __launch_bounds__(256) void wmsa_finalize_kernel(BwdArgs a, float* __
                                                             float* __restrict__ dscale,
                                                             float* __restrict__ dqb) {
   using K = WinCfg<WIN>;
-  __shared__ float bins[K::R * K::R];
   const int h = blockIdx.x;
+  float* acc = a.dbias_acc + (size_t)h * K::TAB;
+  __shared__ float bins[K::R * K::R];
   for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) bins[i] = 0.f;
   __syncthreads();
-  float* acc = a.dbias_acc + (size_t)h * K::TAB;
   for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
     const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
     const int qi = blk / K::NT, ki = blk % K::NT;
@@ -602,9 +621,13 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
     constexpr size_t plds = PairCfg<WIN>::LDS;
     static bool pattr = false;
     if (!pattr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, false>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, false, false>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, true>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, true, false>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, false, true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wmsa_bwd_pair_kernel<WIN, true, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
       pattr = true;
     }
@@ -626,12 +649,17 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
       s.qkv += b0 * tok * 3 * a.g.C;
       s.dout += b0 * tok * a.g.C;
       s.dqkv += b0 * tok * 3 * a.g.C;
+      if (s.rn) s.rn += b0 * tok * 2 * a.g.nH;
       const int it = s.g.n_chunks * s.g.nH;
       const int nb = s.g.xcd_runs ? 8 * ((it + 7) / 8) : (s.g.n_chunks + 7) / 8 * 8 * s.g.nH;
-      if (qnt)
-        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, true>), dim3(nb), dim3(kThreads), plds, st, s);
+      if (qnt && s.rn)
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, true, true>), dim3(nb), dim3(kThreads), plds, st, s);
+      else if (qnt)
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, true, false>), dim3(nb), dim3(kThreads), plds, st, s);
+      else if (s.rn)
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, false, true>), dim3(nb), dim3(kThreads), plds, st, s);
       else
-        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, false>), dim3(nb), dim3(kThreads), plds, st, s);
+        HVK_LAUNCH_TIMED(HVK_TIMER_WMSA_BWD, (wmsa_bwd_pair_kernel<WIN, false, false>), dim3(nb), dim3(kThreads), plds, st, s);
     }
   }
   HVK_CHECK_LAUNCH("wmsa_bwd");
@@ -666,12 +694,18 @@ size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
   return (acc + (size_t)num_heads * 33) * sizeof(float);
 }
 
-int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
-                 int B, int H, int W, int C, int num_heads, int window, int shift,
-                 void* stream) {
+}  // extern "C"
+
+namespace {
+int wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
+             int B, int H, int W, int C, int num_heads, int window, int shift, int normed,
+             void* stream) {
   if (!qkv || !out || !bias_table || !scale)
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_fwd: null pointer");
-  FwdArgs a;
+  if (normed && hvk_wmsa::large_window(window))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_fwd_normed: windows <= 8 only (got %d)", window);
+  FwdArgs a{};
+  a.qk_normed = normed;
   a.qkv = static_cast<const hvk_bf16*>(qkv);
   a.out = static_cast<hvk_bf16*>(out);
   a.bias = bias_table;
@@ -695,20 +729,23 @@ int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table
   return hvk_wmsa::win_fwd(a, B, H, W, C, num_heads, window, shift, st);
 }
 
-int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float* lse, void* dqkv,
-                 float* dq_bias, const float* bias_table, const float* scale,
-                 float* dbias_table, float* dscale, float* workspace, size_t workspace_bytes,
-                 int B, int H, int W, int C, int num_heads, int window, int shift,
-                 void* stream) {
+int wmsa_bwd(const void* qkv, const float* rn, const void* dout, const void* out, const float* lse,
+             void* dqkv, float* dq_bias, const float* bias_table, const float* scale,
+             float* dbias_table, float* dscale, float* workspace, size_t workspace_bytes,
+             int B, int H, int W, int C, int num_heads, int window, int shift,
+             void* stream) {
   if (!qkv || !dout || !dqkv || !bias_table || !scale || !dbias_table || !dscale || !workspace)
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: null pointer");
+  if (rn && hvk_wmsa::large_window(window))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd_normed: windows <= 8 only (got %d)", window);
   if (lse && !out) return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: lse given without the forward's output");
   if (workspace_bytes < hvk_wmsa_bwd_workspace_bytes(num_heads, window))
     return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd: workspace too small");
   // every form addresses one image's qkv rows with 32-bit byte offsets and token rows as int
   if ((long long)H * W * C * 6 >= (1ll << 32) || (long long)B * H * W >= (1ll << 31))
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: %d x %d x %d x %d past 32-bit offsets", B, H, W, C);
-  BwdArgs a;
+  BwdArgs a{};
+  a.rn = rn;
   a.qkv = static_cast<const hvk_bf16*>(qkv);
   a.dout = static_cast<const hvk_bf16*>(dout);
   a.dqkv = static_cast<hvk_bf16*>(dqkv);
@@ -745,6 +782,36 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
     default:
       return hvk_set_error(HVK_EUNSUPPORTED, "hvk_wmsa_bwd: window %d not built (4,6,7,8,12,16,24)", window);
   }
+}
+}  // namespace
+
+extern "C" {
+
+int hvk_wmsa_fwd(const void* qkv, void* out, float* lse, const float* bias_table, const float* scale,
+                 int B, int H, int W, int C, int num_heads, int window, int shift, void* stream) {
+  return wmsa_fwd(qkv, out, lse, bias_table, scale, B, H, W, C, num_heads, window, shift, 0, stream);
+}
+
+int hvk_wmsa_fwd_normed(const void* qkv, void* out, const float* bias_table, const float* scale,
+                        int B, int H, int W, int C, int num_heads, int window, int shift, void* stream) {
+  return wmsa_fwd(qkv, out, nullptr, bias_table, scale, B, H, W, C, num_heads, window, shift, 1, stream);
+}
+
+int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float* lse, void* dqkv,
+                 float* dq_bias, const float* bias_table, const float* scale,
+                 float* dbias_table, float* dscale, float* workspace, size_t workspace_bytes,
+                 int B, int H, int W, int C, int num_heads, int window, int shift, void* stream) {
+  return wmsa_bwd(qkv, nullptr, dout, out, lse, dqkv, dq_bias, bias_table, scale, dbias_table, dscale,
+                  workspace, workspace_bytes, B, H, W, C, num_heads, window, shift, stream);
+}
+
+int hvk_wmsa_bwd_normed(const void* qkv, const float* rn, const void* dout, void* dqkv, float* dq_bias,
+                        const float* bias_table, const float* scale, float* dbias_table, float* dscale,
+                        float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
+                        int num_heads, int window, int shift, void* stream) {
+  if (!rn) return hvk_set_error(HVK_EINVAL, "hvk_wmsa_bwd_normed: null rn");
+  return wmsa_bwd(qkv, rn, dout, nullptr, nullptr, dqkv, dq_bias, bias_table, scale, dbias_table, dscale,
+                  workspace, workspace_bytes, B, H, W, C, num_heads, window, shift, stream);
 }
 
 }  // extern "C"

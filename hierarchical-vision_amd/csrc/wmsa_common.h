@@ -165,6 +165,7 @@ struct FwdArgs {
   WmsaGeom g;
   FastDiv fd_groups, fd_img, fd_ww;  // wmsa_win.hip: / (nH / HG), / (nWh nWw), / nWw
   int dma_nt;                         // wmsa_win.hip: slab DMA with the nontemporal hint
+  int qk_normed;             // 1: q and k head slices arrive L2-normalised (the qkv GEMM's EPI 4)
 };
 
 struct BwdArgs {
@@ -180,6 +181,8 @@ struct BwdArgs {
                              // large windows: [nH, R*R] bins
   float* dscale_acc;         // [nH]
   float* dqb_acc;            // [C]   column sums of dq (q_bias gradient)
+  const float* rn;           // [T, 2nH] 1/max(||q||, eps), 1/max(||k||, eps) when q and k arrive
+                             // normalised (windows <= 8), null for raw q and k
   WmsaGeom g;
 };
 

@@ -12,7 +12,7 @@
 // build reaches 0.65 of 8 TB/s.  Here the hardware starts a new workgroup the moment one ends,
 // each with its whole window in flight at once, and the output leaves as contiguous rows from
 // LDS instead of 64-B per-head pieces from registers (tools/probe/wmsa_mem.hip `win1 glds nt`:
-// 0.80 memory-only, 0.74 with a stand-in for the math).  The per-window setup the ring kernel
+// 0.80 memory-only, 0.74 with a stand-in for the math; profiles/round4/wmsa_fwd_mem_probe_stage0.txt).  The per-window setup the ring kernel
 // amortised (bias table, head bound) overlaps the DMA: its global reads are issued first and
 // waited for by count while the slab is still in flight.
 #include <stdio.h>
@@ -301,10 +301,15 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   static_assert(MM != 1 || (WIN == 7 && K::PW == 8), "the tile-uniform mask form is w7 / shift 3 only");
   const float colmask = (edge_c && (((li >> 2) ^ gq) & 1)) ? mask2 : 0.f;  // query x >= 4 vs key x >= 4
   float rn;
+  if (a.qk_normed) {  // q^ and k^ from the qkv GEMM's epilogue: only the logit scale left
 #pragma unroll
-  for (int i = 0; i < K::NT; ++i) {
-    qf[i] = l2_normalize(qf[i], rn, sc2);
-    kf[i] = l2_normalize(kf[i], rn);
+    for (int i = 0; i < K::NT; ++i) qf[i] = hvk_scale8(qf[i], sc2);
+  } else {
+#pragma unroll
+    for (int i = 0; i < K::NT; ++i) {
+      qf[i] = l2_normalize(qf[i], rn, sc2);
+      kf[i] = l2_normalize(kf[i], rn);
+    }
   }
   // the query-tile loop is instantiated twice, for windows with and without a shift mask: the
   // branch sits outside it, so nothing inside merges registers from two paths

@@ -41,6 +41,9 @@ class GradientBuckets:
         # grad_accum: microbatches before the last only accumulate into the bucket views (no
         # arrival count, no all-reduce: composer's DDP no_sync)
         self.accumulating = False
+        # measurement only (tools/ddp_trace.py): a list -> each bucket's all-reduce enqueue is
+        # marked by a timing event on the producing stream, (bucket, event) appended
+        self.trace = None
         self.buckets = []
         self._hooks = []
         if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
@@ -87,6 +90,10 @@ class GradientBuckets:
             self._pending[bi] -= 1
             if self._pending[bi] == 0 and self.enabled and not self.defer:
                 flat = self.buckets[bi][0]
+                if self.trace is not None:
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    self.trace.append((bi, ev))
                 self._works[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg,
                                                   async_op=True)
         return hook

@@ -318,6 +318,146 @@ def linear(x, weight, bias=None):
     return LinearFn.apply(x, weight, bias)
 
 
+def qkv_nt(x2, wb, bias):
+    """(qkv^, rn) for the qkv Linear of a w <= 8 block: y = x2 wb^T + bias with every q and k
+    head slice L2-normalised (the F.normalize of swinv2.py:229) and rn [M, 2N/96] = their
+    1 / max(||x||, eps), in the GEMM's epilogue where it is built (hvk_linear_qkv_fwd /
+    hvk_gemm_qkv_fwd), else mm_nt + hvk_qk_normalize in place."""
+    M, K = x2.shape
+    N = wb.shape[0]
+    lib = _lib.load()
+    y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
+    rn = torch.empty((M, 2 * N // 96), device=x2.device, dtype=torch.float32)
+    b = ptr(_f32(bias)) if bias is not None else None
+    if _tile_ok(M, K, N) and not _skinny_first(M, K, N) and N % 96 == 0:
+        call("hvk_gemm_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), M, K, N, stream())
+    elif _linear_native(M, K, N) and lib.hvk_linear_qkv_supported(M, K, N):
+        call("hvk_linear_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), M, K, N, stream())
+    else:
+        y = mm_nt(x2, wb, bias)
+        call("hvk_qk_normalize", ptr(y), ptr(rn), M, N // 3, stream())
+    return y, rn
+
+
+class LinearQkvFn(torch.autograd.Function):
+    """The qkv Linear with the q / k normalisation of the attention that consumes it
+    (swinv2.py:220 + 229): returns (qkv^, rn), see qkv_nt.  Its only consumer,
+    WindowAttentionCore with rn, returns the gradient with respect to the UN-normalised qkv
+    (hvk_wmsa_bwd_normed applies the normalisation's backward), so the backward here is
+    LinearFn's."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        xb = _bf16(x)
+        wb, wt = _bf16_weight(weight)
+        N, K = wb.shape
+        y, rn = qkv_nt(xb.reshape(-1, K), wb, bias)
+        ctx.save_for_backward(xb, wb)
+        ctx.wt = wt
+        ctx.has_bias = bias is not None
+        ctx.mark_non_differentiable(rn)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for rn (one fill per block)
+        return y.reshape(*xb.shape[:-1], N), rn
+
+    @staticmethod
+    def backward(ctx, gy, grn):
+        if gy is None:
+            return None, None, None
+        return LinearFn.backward(ctx, gy)
+
+
+def linear_qkv(x, weight, bias=None):
+    return LinearQkvFn.apply(x, weight, bias)
+
+
+# --------------------------------------------------------------------------- classifier head
+_HEAD_WS = {}
+
+
+class HeadFn(torch.autograd.Function):
+    """The classifier head (swinv2.py:786-794) or the multitask tiers (hierarchy.py:19-47) as
+    ONE libhvk GEMM over their concatenated classes (hvk_head_fwd / hvk_head_bwd): logits
+    [M, N_t] per tier (views of one [M, N_pad] bf16 output, N_pad = sum N_t rounded up to 8 with
+    zero weight rows), f32 dW / db straight from the kernels.  x: [M, K] pooled features."""
+
+    @staticmethod
+    def forward(ctx, x, n_w, *wb):
+        ws, bs = wb[:n_w], wb[n_w:]
+        xb = _bf16(x).contiguous()
+        M, K = xb.shape
+        sizes = [w.shape[0] for w in ws]
+        N = sum(sizes)
+        Np = (N + 7) // 8 * 8
+        wcat = [_bf16_weight(w)[0] for w in ws]
+        if Np != N:
+            wcat.append(torch.zeros((Np - N, K), device=xb.device, dtype=torch.bfloat16))
+        wcat = wcat[0] if len(wcat) == 1 else torch.cat(wcat, dim=0)
+        has_b = all(b is not None for b in bs) and len(bs) == n_w
+        bcat = None
+        if has_b:
+            bl = [_f32(b) for b in bs] + ([torch.zeros(Np - N, device=xb.device)] if Np != N else [])
+            bcat = bl[0] if len(bl) == 1 else torch.cat(bl)
+        y = torch.empty((M, Np), device=xb.device, dtype=torch.bfloat16)
+        call("hvk_head_fwd", ptr(xb), ptr(wcat), ptr(bcat) if has_b else None, ptr(y), M, K, Np, stream())
+        ctx.save_for_backward(xb, wcat)
+        ctx.sizes, ctx.Np, ctx.has_b, ctx.n_w = sizes, Np, has_b, n_w
+        ctx.x_dtype = x.dtype
+        outs, off = [], 0
+        for n in sizes:
+            outs.append(y[:, off:off + n])
+            off += n
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        xb, wcat = ctx.saved_tensors
+        M, K = xb.shape
+        sizes, Np = ctx.sizes, ctx.Np
+        parts = [(_bf16(g) if g is not None else torch.zeros((M, n), device=xb.device, dtype=torch.bfloat16))
+                 for g, n in zip(gys, sizes)]
+        if Np != sum(sizes):
+            parts.append(torch.zeros((M, Np - sum(sizes)), device=xb.device, dtype=torch.bfloat16))
+        g = parts[0].contiguous() if len(parts) == 1 else torch.cat(parts, dim=1)
+        want_x = ctx.needs_input_grad[0]
+        want_w = any(ctx.needs_input_grad[2:2 + ctx.n_w])
+        want_b = ctx.has_b and any(ctx.needs_input_grad[2 + ctx.n_w:])
+        gx = torch.empty((M, K), device=xb.device, dtype=torch.float32) if want_x else None
+        dw = torch.empty((Np, K), device=xb.device, dtype=torch.float32) if (want_w or want_b) else None
+        db = torch.empty(Np, device=xb.device, dtype=torch.float32) if want_b else None
+        nb = _lib.load().hvk_head_bwd_workspace_bytes(M, K, Np) if want_x else 0
+        key = (xb.device, nb)
+        wsb = _HEAD_WS.get(key)
+        if nb and wsb is None:
+            wsb = _HEAD_WS[key] = torch.empty(nb // 4, device=xb.device, dtype=torch.float32)
+        call("hvk_head_bwd", ptr(g), ptr(xb), ptr(wcat), ptr(gx) if want_x else None, ptr(dw) if dw is not None else None,
+             ptr(db) if want_b else None, M, K, Np, ptr(wsb) if nb else None, nb, stream())
+        dws, dbs, off = [], [], 0
+        for n in sizes:
+            dws.append(dw[off:off + n] if want_w else None)
+            dbs.append(db[off:off + n] if want_b else None)
+            off += n
+        if not ctx.has_b:
+            dbs = [None] * (len(ctx.needs_input_grad) - 2 - ctx.n_w)
+        gx = gx.to(ctx.x_dtype) if want_x and ctx.x_dtype != torch.float32 else gx
+        return (gx, None, *dws, *dbs)
+
+
+def head_supported(x, weights):
+    """True when the libhvk head GEMMs take this head: CUDA, 2-D features, K % 8 == 0."""
+    if not x.is_cuda or x.dim() != 2:
+        return False
+    K = x.shape[1]
+    N = (sum(w.shape[0] for w in weights) + 7) // 8 * 8
+    return bool(_lib.load().hvk_head_supported(x.shape[0], K, N))
+
+
+def head_linear(x, weights, biases):
+    """Logits of every head Linear (weights[t] [N_t, K], biases[t] [N_t] or None) in one GEMM:
+    a tuple of bf16 [M, N_t] (views of one buffer)."""
+    bs = list(biases) if all(b is not None for b in biases) else []
+    return HeadFn.apply(x, len(weights), *weights, *bs)
+
+
 # --------------------------------------------------------------------------- block biases
 class AttnBiasFn(torch.autograd.Function):
     """(qkv GEMM bias (q_bias, 0, 0), proj bias + W_proj v_bias) of a W-MSA block in ONE
@@ -394,7 +534,7 @@ class WindowAttentionCore(torch.autograd.Function):
     anyway as proj's saved input) instead of recomputing the row statistics."""
 
     @staticmethod
-    def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift):
+    def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift, rn=None):
         B, L, C3 = qkv.shape
         C = C3 // 3
         if L != H * W:
@@ -403,6 +543,13 @@ class WindowAttentionCore(torch.autograd.Function):
         bias_table = _f32(bias_table)
         scale = _f32(scale)
         out = torch.empty((B, L, C), device=qkv.device, dtype=torch.bfloat16)
+        ctx.geom = (B, H, W, C, num_heads, window, shift)
+        ctx.has_q_bias = q_bias is not None
+        if rn is not None:  # q^, k^ from linear_qkv
+            call("hvk_wmsa_fwd_normed", ptr(qkv), ptr(out), ptr(bias_table), ptr(scale), B, H, W, C,
+                 num_heads, window, shift, stream())
+            ctx.save_for_backward(qkv, bias_table, scale, rn)
+            return out
         keep = _WMSA_LARGE_LSE and window > 8
         lse = torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32) if keep else None
         call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(lse), ptr(bias_table), ptr(scale), B, H, W, C,
@@ -411,16 +558,16 @@ class WindowAttentionCore(torch.autograd.Function):
             ctx.save_for_backward(qkv, bias_table, scale, out, lse)
         else:
             ctx.save_for_backward(qkv, bias_table, scale)
-        ctx.geom = (B, H, W, C, num_heads, window, shift)
-        ctx.has_q_bias = q_bias is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
         saved = ctx.saved_tensors
         qkv, bias_table, scale = saved[:3]
-        out, lse = saved[3:] if len(saved) == 5 else (None, None)
         B, H, W, C, nh, win, shift = ctx.geom
+        if len(saved) == 4:
+            return WindowAttentionCore._backward_normed(ctx, dout, qkv, bias_table, scale, saved[3])
+        out, lse = saved[3:] if len(saved) == 5 else (None, None)
         dout = _bf16(dout)
         dqkv = torch.empty_like(qkv)
         dtab = torch.empty_like(bias_table)
@@ -432,12 +579,30 @@ class WindowAttentionCore(torch.autograd.Function):
         call("hvk_wmsa_bwd", ptr(qkv), ptr(dout), ptr(out), ptr(lse), ptr(dqkv),
              ptr(dqb) if dqb is not None else None, ptr(bias_table), ptr(scale), ptr(dtab),
              ptr(dscale), ptr(ws), ws_bytes, B, H, W, C, nh, win, shift, stream())
-        return dqkv, dqb, dtab, dscale, None, None, None, None, None
+        return dqkv, dqb, dtab, dscale, None, None, None, None, None, None
+
+    @staticmethod
+    def _backward_normed(ctx, dout, qkv, bias_table, scale, rn):
+        B, H, W, C, nh, win, shift = ctx.geom
+        dout = _bf16(dout)
+        dqkv = torch.empty_like(qkv)
+        dtab = torch.empty_like(bias_table)
+        dscale = torch.empty_like(scale)
+        dqb = (torch.empty(C, device=qkv.device, dtype=torch.float32)
+               if ctx.has_q_bias and ctx.needs_input_grad[1] else None)
+        ws_bytes = _lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
+        ws = _wmsa_workspace(qkv.device, ws_bytes)
+        call("hvk_wmsa_bwd_normed", ptr(qkv), ptr(rn), ptr(dout), ptr(dqkv),
+             ptr(dqb) if dqb is not None else None, ptr(bias_table), ptr(scale), ptr(dtab),
+             ptr(dscale), ptr(ws), ws_bytes, B, H, W, C, nh, win, shift, stream())
+        return dqkv, dqb, dtab, dscale, None, None, None, None, None, None
 
 
-def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift, q_bias=None):
+def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift, q_bias=None, rn=None):
+    """rn given: qkv holds (q^, k^, v) from linear_qkv (windows <= 8) and the gradient returned
+    for it is the one with respect to the un-normalised qkv."""
     return WindowAttentionCore.apply(qkv, q_bias, bias_table, scale, H, W, num_heads, window,
-                                     shift)
+                                     shift, rn)
 
 
 # --------------------------------------------------------------------------- CPB table

@@ -243,10 +243,14 @@ class WindowAttention(nn.Module):
         if biases is None:
             biases = self.block_tables()
         qkv_b, proj_b = biases[:2]
-        qkv = ops.linear(x, self.qkv.weight, qkv_b)
         table, scale = biases[2:] if len(biases) == 4 else self.cpb_tables()
+        if _QK_EPILOGUE and self.window_size[0] <= 8:
+            # q / k normalisation (swinv2.py:229) in the qkv GEMM's epilogue
+            qkv, rn = ops.linear_qkv(x, self.qkv.weight, qkv_b)
+        else:
+            qkv, rn = ops.linear(x, self.qkv.weight, qkv_b), None
         o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
-                                      self.window_size[0], shift, q_bias=self.q_bias)
+                                      self.window_size[0], shift, q_bias=self.q_bias, rn=rn)
         return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None))
 
     def forward(self, x, mask=None):
@@ -497,6 +501,11 @@ class PatchEmbed(nn.Module):
 
 
 _FUSED_TABLES = os.environ.get("HVK_BLOCK_TABLES", "1") != "0"  # 0: separate launches (A/B runs)
+# windows <= 8: q / k normalised in the qkv GEMM's epilogue, the W-MSA kernels take q^, k^ (and
+# the backward 1/||q||, 1/||k||) as they are (0: raw qkv, the kernels normalise; A/B runs)
+_QK_EPILOGUE = os.environ.get("HVK_QK_EPILOGUE", "1") != "0"
+# the classifier / multitask head on libhvk's head GEMMs (0: ops.linear / the library GEMM, A/B runs)
+_HEAD_GEMM = os.environ.get("HVK_HEAD_GEMM", "1") != "0"
 
 
 def _lib_ln_pool_ok(C):
@@ -637,6 +646,8 @@ class SwinTransformerV2(nn.Module):
         """The classifier: a single Linear runs as ops.linear under autocast (the step's
         prepared bf16 weight, f32 dW straight from the GEMM, no per-call casts)."""
         if isinstance(self.head, nn.Linear) and x.is_cuda and torch.is_autocast_enabled():
+            if _HEAD_GEMM and ops.head_supported(x, [self.head.weight]):
+                return ops.head_linear(x, [self.head.weight], [self.head.bias])[0]
             return ops.linear(x, self.head.weight, self.head.bias)
         return self.head(x)
 

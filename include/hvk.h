@@ -42,7 +42,9 @@ const char* hvk_last_error_string(void);
  *                         (default 2^31, the buffer-descriptor range)
  *   gemm_pp               tiled GEMM kernel choice (hvk_gemm_set_pp below), default 0
  *   tile_wide             tiled GEMM: -1 (default) tile width by shape, 0 128, 1 192 columns
- *   dw_tile               weight gradient at 192-multiple shapes: tile variant 4..8 (default 5) */
+ *   dw_tile               weight gradient at 192-multiple shapes: tile variant 4..8 (default 5)
+ *   gemm_xr               tiled GEMM: 0 (default) tile kernel, 1 / 2 the persistent row-range
+ *                         kernel (gemm_xr.hip; bit-identical, measured slower) */
 int hvk_set_option(const char* name, long long value, long long* previous);
 int hvk_get_option(const char* name, long long* value);
 
@@ -98,6 +100,25 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
                  float* dq_bias, const float* bias_table, const float* scale, float* dbias_table,
                  float* dscale, float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
                  int num_heads, int window, int shift, void* stream);
+/* The w <= 8 pair with the q and k normalisation of swinv2.py:229 done upstream, by the qkv
+ * Linear's epilogue (hvk_linear_qkv_fwd / hvk_gemm_qkv_fwd) or hvk_qk_normalize: qkv holds
+ * (q^, k^, v) with q^ = F.normalize(q), k^ = F.normalize(k) per head, rounded to bf16, and
+ * rn: f32 [B*H*W, 2 num_heads] = 1 / max(||q||, 1e-12) (columns 0..nH-1) and 1 / max(||k||,
+ * 1e-12) (nH..2nH-1) of the un-normalised bf16 q, k.  The backward returns dqkv with respect
+ * to the UN-normalised q, k (the normalisation's backward is applied with rn), so the qkv
+ * Linear's backward is unchanged.  Windows 4, 6, 7, 8 only (EUNSUPPORTED otherwise).  The
+ * backward's q^, k^ and rn equal what hvk_wmsa_bwd computes from raw q, k bit for bit, so
+ * both give the same dqkv; the forward's q^ * scale is rounded twice (q^, then q^ * scale)
+ * instead of once. */
+int hvk_wmsa_fwd_normed(const void* qkv, void* out, const float* bias_table, const float* scale,
+                        int B, int H, int W, int C, int num_heads, int window, int shift, void* stream);
+int hvk_wmsa_bwd_normed(const void* qkv, const float* rn, const void* dout, void* dqkv, float* dq_bias,
+                        const float* bias_table, const float* scale, float* dbias_table, float* dscale,
+                        float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
+                        int num_heads, int window, int shift, void* stream);
+/* In place: every 32-wide q and k head slice of qkv [T, C3 = 3C] (columns < 2C) normalised and
+ * rn [T, 2C/32] written, exactly as the qkv epilogues do (for a qkv produced elsewhere). */
+int hvk_qk_normalize(void* qkv, float* rn, int T, int C, void* stream);
 
 /* ---- Skinny Linear (memory-bound GEMM) ------------------------------------------------
  * y[M, N] = x[M, K] w[N, K]^T (+ bias[N]), bf16 in/out, f32 accumulation: F.linear of
@@ -112,6 +133,16 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
 /* fc1 with its activation fused (swinv2.py:58-62): h = bf16(x w^T + bias) (kept for the
  * backward, = the reference's fc1 output) and y = GELU(h) (exact erf, bf16); replaces
  * hvk_linear_fwd + hvk_bias_gelu_fwd where hvk_linear_gelu_supported(). */
+/* The qkv Linear of a w <= 8 block (swinv2.py:220 + the F.normalize of 229): y = x w^T + bias
+ * (N = 3K) with the q and k head slices normalised and rn [M, 2K/32] written (see
+ * hvk_wmsa_fwd_normed); the v slice is hvk_linear_fwd's bit for bit.  Built for K = 96, 128,
+ * 192, 256 (hvk_linear_qkv_supported); hvk_gemm_qkv_fwd is the tiled form (N % 96 == 0,
+ * hvk_gemm_supported shapes). */
+int hvk_linear_qkv_supported(int M, int K, int N);
+int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
+                       int N, void* stream);
+int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
+                     int N, void* stream);
 int hvk_linear_gelu_supported(int M, int K, int N);
 int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                         int K, int N, void* stream);
@@ -187,6 +218,20 @@ int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, i
 int hvk_weight_grad_gelu_x_supported(int M, int N, int K);
 int hvk_weight_grad_gelu_x(const void* g, const void* h, float* dw, float* db, int M, int N, int K, void* ws,
                            size_t ws_bytes, void* stream);
+
+/* ---- Classifier head (M = the batch) ---------------------------------------------------
+ * The head Linear of swinv2.py:786-794 and the concatenated tiers of the multitask head
+ * (hierarchy.py:19-47): M rows of pooled features, N classes (10 000 leaves for HXE), neither a
+ * tile multiple.  x: bf16 [M, K]; w: bf16 [N, K]; bias: f32 [N] or NULL; y: bf16 [M, N] =
+ * bf16(x w^T + bias).  K and N multiples of 8 (hvk_head_supported); the caller pads a class
+ * count that is not (zero weight rows).  Backward: g = bf16 [M, N] gradient of y; gx: f32
+ * [M, K] = g w (or NULL: needs the workspace of hvk_head_bwd_workspace_bytes); dw: f32 [N, K] =
+ * g^T x and db: f32 [N] = column sums of g (or NULL), all overwritten. */
+int hvk_head_supported(int M, int K, int N);
+int hvk_head_fwd(const void* x, const void* w, const float* bias, void* y, int M, int K, int N, void* stream);
+size_t hvk_head_bwd_workspace_bytes(int M, int K, int N);
+int hvk_head_bwd(const void* g, const void* x, const void* w, float* gx, float* dw, float* db, int M, int K,
+                 int N, float* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- bf16 weight copies for a step --------------------------------------------------
  * For k < n: dst[k] = bf16(src[k]) ([rows[k], cols[k]] row-major, f32 -> bf16 round to

@@ -1,0 +1,242 @@
+"""q / k head normalisation moved into the qkv Linear (swinv2.py:220 + 229): the epilogue forms
+(hvk_linear_qkv_fwd, hvk_gemm_qkv_fwd) against the plain GEMM + the standalone normalisation
+(bit for bit), the normalisation against torch's F.normalize (fp32, tolerance in the test), and
+the W-MSA pair that consumes q^, k^ (hvk_wmsa_fwd_normed / hvk_wmsa_bwd_normed) against the raw
+form: the backward bit for bit, the forward within one extra bf16 rounding of q^ * scale."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import swinv2_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    import hvamd._lib as lib
+    return lib
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int16)
+
+
+def _qk_ref(qkv, C):
+    """(q^, k^ per 32-wide head, rn) in fp32 from bf16 qkv [T, 3C]: F.normalize(eps=1e-12)."""
+    T = qkv.shape[0]
+    x = qkv.float()[:, :2 * C].reshape(T, 2 * C // 32, 32)
+    norm = x.norm(dim=-1)
+    return F.normalize(x, dim=-1).reshape(T, 2 * C), 1.0 / norm.clamp_min(1e-12)
+
+
+@pytest.mark.parametrize("T,C", [(1000, 96), (37, 192), (4096, 384), (16, 32), (517, 768)])
+def test_qk_normalize_matches_torch(T, C):
+    lib = _lib()
+    g = torch.Generator(device="cuda").manual_seed(T + C)
+    qkv = (3 * torch.randn(T, 3 * C, device="cuda", generator=g)).bfloat16()
+    qkv[5 % T, :32] = 0  # a zero q head: F.normalize gives 0, rn = 1 / eps
+    src = qkv.clone()
+    rn = torch.empty(T, 2 * C // 32, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(qkv), lib.ptr(rn), T, C, lib.stream())
+    torch.cuda.synchronize()
+    ref, rn_ref = _qk_ref(src, C)
+    assert torch.equal(_bits(qkv[:, 2 * C:]), _bits(src[:, 2 * C:])), "v slice changed"
+    got = qkv[:, :2 * C].float()
+    # one bf16 rounding of the normalised value (2^-8 relative) on unit-norm 32-vectors
+    assert (got - ref).abs().max().item() < 8e-3
+    assert torch.allclose(rn, rn_ref, rtol=2e-6, atol=0), (rn - rn_ref).abs().max()
+
+
+SKINNY = [(96, 288), (192, 576), (128, 384), (256, 768)]
+TILED = [(192, 576), (384, 1152), (768, 2304)]
+
+
+def _gemm_case(M, K, N, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g)
+    b[N // 3:] = 0  # the qkv GEMM's bias is (q_bias, 0, 0)
+    return x, w, b
+
+
+@pytest.mark.parametrize("M", [4099, 50176])
+@pytest.mark.parametrize("K,N", SKINNY)
+def test_linear_qkv_epilogue_bit_identical(M, K, N):
+    lib = _lib()
+    assert lib.load().hvk_linear_qkv_supported(M, K, N)
+    x, w, b = _gemm_case(M, K, N, M + K)
+    y0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    lib.call("hvk_linear_fwd", lib.ptr(x), lib.ptr(w), lib.ptr(b), lib.ptr(y0), M, K, N, lib.stream())
+    rn0 = torch.empty(M, 2 * N // 96, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(y0), lib.ptr(rn0), M, N // 3, lib.stream())
+    y1 = torch.empty_like(y0)
+    rn1 = torch.full_like(rn0, float("nan"))
+    lib.call("hvk_linear_qkv_fwd", lib.ptr(x), lib.ptr(w), lib.ptr(b), lib.ptr(y1), lib.ptr(rn1), M, K, N,
+             lib.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(_bits(y0), _bits(y1))
+    assert torch.equal(rn0.view(torch.int32), rn1.view(torch.int32))
+
+
+@pytest.mark.parametrize("M", [12544, 4160])
+@pytest.mark.parametrize("K,N", TILED)
+@pytest.mark.parametrize("wide", [-1, 0, 1])
+def test_gemm_qkv_epilogue_bit_identical(M, K, N, wide):
+    lib = _lib()
+    if wide == 0 and N % 128:
+        pytest.skip("128-column tile needs 128 | N")
+    x, w, b = _gemm_case(M, K, N, M + K + 7)
+    y0 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    lib.call("hvk_gemm_fwd", lib.ptr(x), lib.ptr(w), lib.ptr(b), lib.ptr(y0), M, K, N, lib.stream())
+    rn0 = torch.empty(M, 2 * N // 96, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(y0), lib.ptr(rn0), M, N // 3, lib.stream())
+    y1 = torch.empty_like(y0)
+    rn1 = torch.full_like(rn0, float("nan"))
+    with lib.option("tile_wide", wide):
+        lib.call("hvk_gemm_qkv_fwd", lib.ptr(x), lib.ptr(w), lib.ptr(b), lib.ptr(y1), lib.ptr(rn1), M, K, N,
+                 lib.stream())
+        torch.cuda.synchronize()
+    assert torch.equal(_bits(y0), _bits(y1))
+    assert torch.equal(rn0.view(torch.int32), rn1.view(torch.int32))
+
+
+WCASES = [(2, 14, 14, 2, 7, 3), (3, 56, 56, 3, 7, 3), (2, 7, 7, 24, 7, 0), (2, 16, 16, 2, 8, 4),
+          (1, 12, 12, 4, 6, 3), (2, 8, 8, 2, 4, 2), (1, 21, 14, 3, 7, 3), (1, 14, 14, 16, 7, 3)]
+
+
+def _wmsa_inputs(B, H, W, nh, win, seed):
+    rng = np.random.default_rng(seed)
+    C = 32 * nh
+    qkv = torch.from_numpy(rng.standard_normal((B * H * W, 3 * C)).astype(np.float32)).bfloat16().cuda()
+    tab = torch.from_numpy((16 / (1 + np.exp(-rng.standard_normal((nh, (2 * win - 1) ** 2))))).astype(np.float32)).cuda()
+    scale = torch.from_numpy(np.exp(np.minimum(np.log(10) + 0.5 * rng.standard_normal(nh), np.log(100))).astype(np.float32)).cuda()
+    dout = torch.from_numpy(rng.standard_normal((B * H * W, C)).astype(np.float32)).bfloat16().cuda()
+    return qkv, tab, scale, dout
+
+
+@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("B,H,W,nh,win,shift", WCASES)
+def test_wmsa_normed_forward(B, H, W, nh, win, shift, form):
+    """Normed forward vs the raw one on the same qkv and vs the fp32 oracle."""
+    lib = _lib()
+    C = 32 * nh
+    qkv, tab, scale, _ = _wmsa_inputs(B, H, W, nh, win, 11)
+    qn = qkv.clone()
+    rn = torch.empty(B * H * W, 2 * nh, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(qn), lib.ptr(rn), B * H * W, C, lib.stream())
+    o_raw = torch.empty(B * H * W, C, device="cuda", dtype=torch.bfloat16)
+    o_n = torch.empty_like(o_raw)
+    with lib.option("wmsa_fwd_form", form):
+        lib.call("hvk_wmsa_fwd", lib.ptr(qkv), lib.ptr(o_raw), None, lib.ptr(tab), lib.ptr(scale), B, H, W, C,
+                 nh, win, shift, lib.stream())
+        lib.call("hvk_wmsa_fwd_normed", lib.ptr(qn), lib.ptr(o_n), lib.ptr(tab), lib.ptr(scale), B, H, W, C,
+                 nh, win, shift, lib.stream())
+        torch.cuda.synchronize()
+    ref = swinv2_ref.wmsa_core_ref(qkv.float().cpu().reshape(B, H * W, 3 * C), tab.cpu(), scale.cpu(), H, W,
+                                   nh, win, shift).reshape(B * H * W, C)
+    rels, maxs = [], []
+    for o in (o_raw, o_n):
+        o = o.float().cpu()
+        rels.append(((o - ref).norm() / ref.norm()).item())
+        maxs.append((o - ref).abs().max().item())
+    # the normed form rounds q^ * scale twice (q^ to bf16 in the epilogue, then q^ * scale): its
+    # distance from the fp32 oracle stays that of the raw form (logit scales up to 100 amplify
+    # either rounding alike; test_gpu_wmsa.py holds the raw form to the oracle)
+    assert rels[1] < 1e-2 and rels[1] <= 1.25 * rels[0] + 1e-3, rels
+    assert maxs[1] <= 1.5 * maxs[0] + 1e-2, maxs
+
+
+@pytest.mark.parametrize("B,H,W,nh,win,shift", WCASES)
+def test_wmsa_normed_backward_bit_identical(B, H, W, nh, win, shift):
+    """hvk_wmsa_bwd_normed(q^, k^, rn) == hvk_wmsa_bwd(raw q, k): the kernel's own normalisation
+    and the standalone one are the same instruction sequence."""
+    lib = _lib()
+    C = 32 * nh
+    qkv, tab, scale, dout = _wmsa_inputs(B, H, W, nh, win, 12)
+    qn = qkv.clone()
+    T = B * H * W
+    rn = torch.empty(T, 2 * nh, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(qn), lib.ptr(rn), T, C, lib.stream())
+    nb = lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
+    ws = torch.zeros(nb // 4, device="cuda")
+    outs = []
+    for normed in (0, 1):
+        dqkv = torch.empty(T, 3 * C, device="cuda", dtype=torch.bfloat16)
+        dqb = torch.empty(C, device="cuda")
+        dtab = torch.empty_like(tab)
+        dsc = torch.empty_like(scale)
+        if normed:
+            lib.call("hvk_wmsa_bwd_normed", lib.ptr(qn), lib.ptr(rn), lib.ptr(dout), lib.ptr(dqkv), lib.ptr(dqb),
+                     lib.ptr(tab), lib.ptr(scale), lib.ptr(dtab), lib.ptr(dsc), lib.ptr(ws), nb, B, H, W, C, nh,
+                     win, shift, lib.stream())
+        else:
+            lib.call("hvk_wmsa_bwd", lib.ptr(qkv), lib.ptr(dout), None, None, lib.ptr(dqkv), lib.ptr(dqb),
+                     lib.ptr(tab), lib.ptr(scale), lib.ptr(dtab), lib.ptr(dsc), lib.ptr(ws), nb, B, H, W, C, nh,
+                     win, shift, lib.stream())
+        torch.cuda.synchronize()
+        outs.append((dqkv, dqb, dtab, dsc))
+    a, b = outs
+    assert torch.equal(_bits(a[0]), _bits(b[0]))
+    # dq_bias, the CPB-table and scale gradients are summed over workgroups with float atomics:
+    # equal up to the summation order
+    for x, y in zip(a[1:], b[1:]):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-5 * y.abs().max().item())
+    assert torch.count_nonzero(ws).item() == 0
+
+
+def test_wmsa_normed_batch_slices():
+    """The normed backward over batch slices (option wmsa_bwd_slice_bytes) == one launch."""
+    lib = _lib()
+    B, H, W, nh, win, shift = 4, 14, 14, 3, 7, 3
+    C, T = 32 * nh, 4 * 14 * 14
+    qkv, tab, scale, dout = _wmsa_inputs(B, H, W, nh, win, 13)
+    rn = torch.empty(T, 2 * nh, device="cuda")
+    lib.call("hvk_qk_normalize", lib.ptr(qkv), lib.ptr(rn), T, C, lib.stream())
+    nb = lib.load().hvk_wmsa_bwd_workspace_bytes(nh, win)
+    ws = torch.zeros(nb // 4, device="cuda")
+    res = []
+    for sl in (1 << 31, H * W * 3 * C * 2 + 1):
+        dqkv = torch.empty(T, 3 * C, device="cuda", dtype=torch.bfloat16)
+        dtab, dsc = torch.empty_like(tab), torch.empty_like(scale)
+        with lib.option("wmsa_bwd_slice_bytes", sl):
+            lib.call("hvk_wmsa_bwd_normed", lib.ptr(qkv), lib.ptr(rn), lib.ptr(dout), lib.ptr(dqkv), None,
+                     lib.ptr(tab), lib.ptr(scale), lib.ptr(dtab), lib.ptr(dsc), lib.ptr(ws), nb, B, H, W, C, nh,
+                     win, shift, lib.stream())
+            torch.cuda.synchronize()
+        res.append(dqkv)
+    assert torch.equal(_bits(res[0]), _bits(res[1]))
+
+
+def test_wmsa_normed_rejects_large_windows():
+    lib = _lib()
+    x = torch.zeros(24 * 24, 3 * 64, device="cuda", dtype=torch.bfloat16)
+    o = torch.zeros(24 * 24, 64, device="cuda", dtype=torch.bfloat16)
+    tab = torch.zeros(2, 23 * 23, device="cuda")
+    sc = torch.ones(2, device="cuda")
+    rc = lib.load().hvk_wmsa_fwd_normed(lib.ptr(x), lib.ptr(o), lib.ptr(tab), lib.ptr(sc), 1, 24, 24, 64, 2, 12,
+                                        6, lib.stream())
+    assert rc == 2
+
+
+def test_block_qk_epilogue_matches_raw(monkeypatch):
+    """One SwinV2 block, forward + backward, with the q / k normalisation in the qkv epilogue vs
+    in the W-MSA kernels: same loss within bf16 noise, gradients close."""
+    import hvamd.swinv2 as sw
+    torch.manual_seed(0)
+    blk = sw.SwinTransformerBlock(96, (28, 28), 3, window_size=7, shift_size=3).cuda()
+    x = torch.randn(4, 28 * 28, 96, device="cuda")
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(sw, "_QK_EPILOGUE", on)
+        blk.zero_grad(set_to_none=True)
+        y = blk(x)
+        loss = y.float().square().mean()
+        loss.backward()
+        res.append((loss.item(), {n: p.grad.clone() for n, p in blk.named_parameters() if p.grad is not None}))
+    (l0, g0), (l1, g1) = res
+    assert abs(l0 - l1) <= 2e-3 * abs(l0)
+    for n in g0:
+        rel = ((g0[n] - g1[n]).norm() / (g0[n].norm() + 1e-12)).item()
+        assert rel < 3e-2, (n, rel)

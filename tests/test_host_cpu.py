@@ -25,7 +25,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib.SIGNATURES), set(declared) ^ set(_lib.SIGNATURES)
     lib = _lib.load()
-    assert lib.hvk_abi_version() == 8
+    assert lib.hvk_abi_version() == 9
     # [accumulators][dscale nH][dq_bias 32 nH] floats
     assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
     assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4

@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--recompute", action="store_true",
                     help="large windows: backward recomputes the row statistics (no forward row constants)")
     ap.add_argument("--b384", action="store_true", help="SwinV2-B 384 w24 stage shapes (config 5)")
+    ap.add_argument("--normed", action="store_true",
+                    help="windows <= 8: q / k normalised upstream (hvk_wmsa_fwd_normed / _bwd_normed, the model's path)")
     args = ap.parse_args()
     from hvamd import _lib
     if args.lib:
@@ -81,15 +83,26 @@ def main():
 
         keep = win > 8 and not args.recompute  # as ops.WindowAttentionCore
         lse = torch.empty(T, nh, device="cuda") if keep else None
+        normed = args.normed and win <= 8
+        rn = torch.empty(T, 2 * nh, device="cuda")
+        if normed:
+            _lib.call("hvk_qk_normalize", P(qkv), P(rn), T, C, st())
 
         def fwd():
-            _lib.call("hvk_wmsa_fwd", P(qkv), P(out), P(lse), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
+            if normed:
+                _lib.call("hvk_wmsa_fwd_normed", P(qkv), P(out), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
+            else:
+                _lib.call("hvk_wmsa_fwd", P(qkv), P(out), P(lse), P(tab), P(scale), B, H, W, C, nh, win, sh, st())
 
         fwd()  # out / lse for the backward
 
         def bwd():
-            _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(out) if keep else None, P(lse), P(dqkv), P(dqb),
-                      P(tab), P(scale), P(dtab), P(dsc), P(ws), wsb, B, H, W, C, nh, win, sh, st())
+            if normed:
+                _lib.call("hvk_wmsa_bwd_normed", P(qkv), P(rn), P(dout), P(dqkv), P(dqb), P(tab), P(scale), P(dtab),
+                          P(dsc), P(ws), wsb, B, H, W, C, nh, win, sh, st())
+            else:
+                _lib.call("hvk_wmsa_bwd", P(qkv), P(dout), P(out) if keep else None, P(lse), P(dqkv), P(dqb),
+                          P(tab), P(scale), P(dtab), P(dsc), P(ws), wsb, B, H, W, C, nh, win, sh, st())
 
         tf = timeit(fwd, args.iters, 0) if args.only != "bwd" else float("nan")
         tb = timeit(bwd, args.iters, 1) if args.only != "fwd" else float("nan")

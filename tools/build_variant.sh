@@ -3,12 +3,16 @@
 # optional extra CXXFLAGS) into abl/<name>.so for A/B runs (tools/gpu_ab_lib.sh).
 #   tools/build_variant.sh HEAD base            # committed kernels
 #   EXTRA="-DHVK_X=1" tools/build_variant.sh WT probe
+#   FROM_REV="HEAD:layernorm.hip" tools/build_variant.sh WT lnold   # one file from a revision
 set -e
 REV=$1; NAME=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d /tmp/hvkvar.XXXX)
 if [ "$REV" = WT ]; then cp -r "$ROOT/hierarchical-vision_amd/csrc/." "$T/"; rm -rf "$T/build"
 else git -C "$ROOT" archive "$REV" hierarchical-vision_amd/csrc | tar -x -C "$T" --strip-components=2; fi
+for fr in $FROM_REV; do
+  git -C "$ROOT" show "${fr%%:*}:hierarchical-vision_amd/csrc/${fr#*:}" > "$T/${fr#*:}"
+done
 mkdir -p "$ROOT/abl"
 make -s -C "$T" -j8 OUT="$ROOT/abl/$NAME.so" CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result $EXTRA"
 rm -rf "$T"

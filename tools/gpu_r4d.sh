@@ -20,3 +20,6 @@ for t in dwqkv fwdqkv; do
     [ -d $d ] && python3 tools/pmc_report.py $d "dw_kernel|gemm_nt|gemm_xr" > gpurun_out/pmc_$t/$p.txt 2>&1 && cat gpurun_out/pmc_$t/$p.txt
   done
 done
+# bucket all-reduce enqueue points against the backward (one-rank RCCL, buckets forced, bs256)
+timeout -k 10 300 python3 tools/ddp_trace.py --batch 256 > gpurun_out/r4d_ddp_enqueue.txt 2>&1 || { tail -20 gpurun_out/r4d_ddp_enqueue.txt; exit 1; }
+cat gpurun_out/r4d_ddp_enqueue.txt

@@ -20,6 +20,7 @@ CATS = [  # (category, regex on the kernel name), first match wins
     ("bias_gelu", r"bias_gelu|colsum_rows"),
     ("patch_merge", r"merge_kernel"),
     ("losses", r"multitask|hxe"),
+    ("head", r"head_kernel|head_sum"),
     ("gemm(dW)", r"dw_kernel|dw_reduce"),
     ("gemm(hvk)", r"linear_kernel|gemm_nt_kernel|gemm_pp_kernel|mlp_fwd_kernel|mlp_bwd_kernel"),
     ("gemm", r"Cijk|gemm|Gemm|GEMM|mfma|MT\d+x\d+"),

@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp || exit 1
-CMD="python3 $R/tools/bench_wmsa.py --iters 3 --stage ${STAGE:-0} --only $ONLY"
+CMD="python3 $R/tools/bench_wmsa.py --iters 3 --stage ${STAGE:-0} --only $ONLY $WMSA_ARGS"
 run() {  # name counters...
   local name=$1; shift
   case ",$PASSES," in *",$name,"*) ;; *) return 0 ;; esac
