@@ -8,7 +8,8 @@
 //   weight grad    dw[N, K] = g^T x, db[N] = sum_m g[m, :] (f32)
 //
 // One kernel form: C[i][j] = sum_c A(i, c) B(j, c) on 64 x 64 output tiles (four waves, 32 x 32
-// each, 16x16x32 bf16 MFMA), the contraction staged through LDS 64 at a time.  An operand whose
+// each, 16x16x32 bf16 MFMA), the contraction staged through registers and LDS 64 at a time (the
+// next block's global reads in flight under the current block's MFMAs).  An operand whose
 // contraction index is not the contiguous one (w in the input gradient, both in the weight
 // gradient) is transposed on its way into LDS (8 two-byte LDS writes per 16-B global read), so
 // every fragment read is one ds_read_b128.  Ragged edges: 8-element chunks past a bound load as
@@ -20,32 +21,48 @@ namespace {
 constexpr int HB = 64;       // output tile rows / columns and contraction chunk
 constexpr int HLD = HB + 8;  // LDS row stride (bf16): rows 16 B apart in bank space
 
-// Stage the [HB x HB] block (rows r0.., contraction c0..) of a logical operand L into LDS as
-// lds[r][c] (stride HLD).  T = false: L(r, c) = g[r * ld + c]; T = true: L(r, c) = g[c * ld + r].
-// R / CE bound r / c; the contiguous index of g comes in whole 8-element chunks.
+// One [HB x HB] block (rows r0.., contraction c0..) of a logical operand L, staged through
+// registers into LDS as lds[r][c] (stride HLD).  T = false: L(r, c) = g[r * ld + c]; T = true:
+// L(r, c) = g[c * ld + r].  R / CE bound r / c; the contiguous index of g comes in whole
+// 8-element chunks.  load() issues the thread's two 16-B global reads, store() writes them
+// (transposed: 8 two-byte LDS writes per read) -- split so the next block's reads are in flight
+// while the current block's MFMAs run.
 template <bool T>
-__device__ __forceinline__ void stage(hvk_bf16* lds, const hvk_bf16* __restrict__ g, int ld, int r0, int c0, int R,
-                                      int CE) {
+struct Stager {
+  uint4 v[2];
+  __device__ __forceinline__ void load(const hvk_bf16* __restrict__ g, int ld, int r0, int c0, int R, int CE) {
 #pragma unroll
-  for (int e = threadIdx.x; e < HB * HB / 8; e += 256) {
-    const int a = e >> 3, b = (e & 7) * 8;  // a: the strided index, b: 8 contiguous ones
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if constexpr (!T) {
-      const int r = r0 + a, c = c0 + b;
-      if (r < R && c < CE) v = hvk_ld16(g + (size_t)r * ld + c);
-      *reinterpret_cast<uint4*>(lds + a * HLD + b) = v;
-    } else {
-      const int c = c0 + a, r = r0 + b;
-      if (c < CE && r < R) v = hvk_ld16(g + (size_t)c * ld + r);
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        lds[(b + 2 * k) * HLD + a] = (hvk_bf16)(w[k] & 0xffff);
-        lds[(b + 2 * k + 1) * HLD + a] = (hvk_bf16)(w[k] >> 16);
+    for (int k = 0; k < 2; ++k) {
+      const int e = threadIdx.x + 256 * k;
+      const int a = e >> 3, b = (e & 7) * 8;  // a: the strided index, b: 8 contiguous ones
+      v[k] = make_uint4(0, 0, 0, 0);
+      if constexpr (!T) {
+        const int r = r0 + a, c = c0 + b;
+        if (r < R && c < CE) v[k] = hvk_ld16(g + (size_t)r * ld + c);
+      } else {
+        const int c = c0 + a, r = r0 + b;
+        if (c < CE && r < R) v[k] = hvk_ld16(g + (size_t)c * ld + r);
       }
     }
   }
-}
+  __device__ __forceinline__ void store(hvk_bf16* lds) const {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = threadIdx.x + 256 * k;
+      const int a = e >> 3, b = (e & 7) * 8;
+      if constexpr (!T) {
+        *reinterpret_cast<uint4*>(lds + a * HLD + b) = v[k];
+      } else {
+        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          lds[(b + 2 * q) * HLD + a] = (hvk_bf16)(w[q] & 0xffff);
+          lds[(b + 2 * q + 1) * HLD + a] = (hvk_bf16)(w[q] >> 16);
+        }
+      }
+    }
+  }
+};
 
 // EPI 0: bf16 out[j][i] = C + bias[i] (the forward, i = class, j = row of the batch);
 // EPI 1: f32 out[z][j][i] = C over contraction slice z (input-gradient partials, weight gradient);
@@ -68,10 +85,20 @@ __global__ __launch_bounds__(256) void head_kernel(const hvk_bf16* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 2; ++u) acc[t][u] = hvk_f32x4{0, 0, 0, 0};
   float dbs = 0.f;
+  Stager<AT> sa;
+  Stager<BT> sb;
+  if (cb < ce) {
+    sa.load(A, lda, i0, cb, I, ce);
+    sb.load(B, ldb, j0, cb, J, ce);
+  }
   for (int c0 = cb; c0 < ce; c0 += HB) {
-    stage<AT>(As, A, lda, i0, c0, I, ce);
-    stage<BT>(Bs, B, ldb, j0, c0, J, ce);
+    sa.store(As);
+    sb.store(Bs);
     __syncthreads();
+    if (c0 + HB < ce) {  // the next block's reads, in flight under this block's MFMAs
+      sa.load(A, lda, i0, c0 + HB, I, ce);
+      sb.load(B, ldb, j0, c0 + HB, J, ce);
+    }
     if (DB && blockIdx.x == 0 && threadIdx.x < HB) {
 #pragma unroll 8
       for (int c = 0; c < HB; ++c) dbs += __uint_as_float((uint32_t)Bs[threadIdx.x * HLD + c] << 16);

@@ -72,6 +72,14 @@ __device__ __forceinline__ void lds_wr128(uint32_t a, uint4 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(__builtin_bit_cast(hvk_u32x4, v)) : "memory");
 }
 
+// Slab swizzle: the 16-B chunk k (0..3) of a head's 64-B segment of token column x sits at chunk
+// k ^ swz(x).  Without it the fragment reads of a wave (16 rows = token columns 0..7 of two
+// window rows, 36-slot token stride) hit each 64-bank group twice and the output write-back four
+// times (39 % of the stage-0 LDS cycles were bank conflicts, profiles/round4/pmc_wmsa_normed);
+// with it both are conflict-free (bank model of MI355X_MICROARCH.md §LDS, every w / HG checked).
+// The DMA places the chunks, every slab reader applies the same XOR.
+__device__ __forceinline__ unsigned swz(unsigned x) { return (x >> 1) & 3u; }
+
 // MM: shift-mask form, fixed at launch so no branch (and no register copies where branches
 // merge) sits in the score loop: 0 unshifted block (no mask), 1 w7 / shift 3 (tile-uniform
 // row band + per-lane column band: one add per element, every window), 2 any other shift
@@ -129,7 +137,8 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       // slot q = RS tx + 4HG part + c with RS = 3 (4HG): u = q / 4HG = 3 tx + part, and the byte
       // offset tx 6C + part 2C = u 2C
       const unsigned u = q / (4 * HG), c = q - mad24(u, 4u * HG, 0u), tx = u / 3;
-      const unsigned v = (__umul24(u, 2u * C) + c * 16 + grp_off) | (tx << 24);
+      const unsigned cs = (c & ~3u) | ((c & 3u) ^ swz(tx));  // the global chunk this slot holds
+      const unsigned v = (__umul24(u, 2u * C) + cs * 16 + grp_off) | (tx << 24);
       pre[k] = q < (unsigned)(WIN * K::RS) ? v : (unsigned)grp_off;
     }
     const char* img = reinterpret_cast<const char*>(a.qkv) + (size_t)b * g.H * WRB;
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
 #if HVK_WIN_PROBE != 1
   const uint32_t zaddr = lds_addr(zero16);
   const int fx = li % K::PW, fy0 = li / K::PW;
-  const uint32_t fb = lds_addr(smem) + (fy0 * K::RUN + fx * K::RS + wave * 4 + gq) * 16;
+  const uint32_t fb = lds_addr(smem) + (fy0 * K::RUN + fx * K::RS + wave * 4 + (gq ^ swz(fx))) * 16;
   hvk_u32x4 qr[K::NT], kr[K::NT];
   hvk_u32x2 vr[K::NC][2][2];
 #pragma unroll
@@ -265,7 +274,8 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   {
     const int pl = 4 * gq + (li >> 2);
     const int x = pl % K::PW, y0 = pl / K::PW;
-    const uint32_t vb = lds_addr(smem) + (y0 * K::RUN + x * K::RS) * 16 + (2 * HG * 32 + wave * 32 + 8 * (li & 3)) * 2;
+    const uint32_t vb =
+        lds_addr(smem) + (y0 * K::RUN + x * K::RS) * 16 + (2 * HG * 32 + wave * 32 + 8 * ((li & 3) ^ swz(x))) * 2;
 #pragma unroll
     for (int c = 0; c < K::NC; ++c)
 #pragma unroll
@@ -479,7 +489,8 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
       const int t = t0 + 16 * k, ty = t / WIN, tx = t - ty * WIN;
       // slots past the window (last round only) read a valid slab address and store nothing
       const uint32_t sl = __umul24((uint32_t)ty, (uint32_t)(K::RUN * 16)) + __umul24((uint32_t)tx, (uint32_t)(K::RS * 16));
-      v[k] = lds_rd128<0>(lds_addr(smem) + (t < K::N ? sl + c * 16 : 0u));
+      const unsigned cs = (c & ~3u) | ((c & 3u) ^ swz(tx));
+      v[k] = lds_rd128<0>(lds_addr(smem) + (t < K::N ? sl + cs * 16 : 0u));
       uint32_t o = mad24(mad24((uint32_t)ty, (uint32_t)g.W, (uint32_t)tx), C2, c * 16u);
       if (wrap) o -= (ty >= ly ? imgb : 0u) + (tx >= lx ? rowb : 0u);
       off[k] = (int)o;  // two's complement: the wrapped offsets come out negative

@@ -161,7 +161,7 @@ def test_patchify_bf16_bit_exact(B, H, W):
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("C", [96, 192, 384, 768, 1024, 64])
+@pytest.mark.parametrize("C", [96, 192, 384, 768, 1024, 64, 48, 128])
 def test_layernorm_residual_vs_torch(C):
     import hvamd.ops as ops
     B, L = 3, 50
