@@ -270,13 +270,6 @@ constexpr int kBwdBlocks = 1024;
 // ln_probe.hip: 8 channels per lane up to C = 512, the fastest at C = 96 / 192 / 384, 16 above)
 int pick_layout(int C, int& ept, int& tpr) {
   if (C % 8) return 1;
-  // C = 12 * 2^k (SwinV2-T's 96 ... 768): 12 channels per lane fill every lane (the 8 / 16 layouts
-  // leave a quarter of them idle at these widths)
-  if (C % 12 == 0 && (C / 12 & (C / 12 - 1)) == 0 && C / 12 >= 8 && C / 12 <= 64) {
-    ept = 12;
-    tpr = C / 12;
-    return 0;
-  }
   ept = C > 512 ? 16 : 8;
   tpr = 1;
   while (tpr * ept < C) tpr <<= 1;
@@ -293,10 +286,6 @@ int pick_layout(int C, int& ept, int& tpr) {
     case 8032: hipLaunchKernelGGL((KERNEL<8, 32>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
     case 8064: hipLaunchKernelGGL((KERNEL<8, 64>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
     case 16064: hipLaunchKernelGGL((KERNEL<16, 64>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break; \
-    case 12008: hipLaunchKernelGGL((KERNEL<12, 8>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break;  \
-    case 12016: hipLaunchKernelGGL((KERNEL<12, 16>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break; \
-    case 12032: hipLaunchKernelGGL((KERNEL<12, 32>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break; \
-    case 12064: hipLaunchKernelGGL((KERNEL<12, 64>), GRID, dim3(64 * kWaves), 0, ST, ARGS); break; \
     default: return hvk_set_error(HVK_EUNSUPPORTED, "layernorm: no layout for C=%d", C);      \
   }
 

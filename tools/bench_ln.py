@@ -58,7 +58,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) / a.iters * 1e3
-            res.append(f"{us:7.1f} us {nbytes / us / 1e6:6.0f} GB/s {nbytes / us / 8e6:.3f}")
+            res.append(f"{us:7.1f} us {nbytes / us / 1e6:5.2f} TB/s {nbytes / us / 8e6:.3f}")
         print(f"{name} C={C:4d}  fwd {res[0]}  | bwd {res[1]}", flush=True)
 
 
