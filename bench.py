@@ -113,13 +113,18 @@ TRAFFIC_SOURCE = ("bench_traffic.json: HBM bytes per launch (mean over the step'
                   "(tools/gpu_traffic.sh); null when that file is absent")
 
 
-def measured_traffic(kernel):
-    """Mean HBM bytes per launch of `kernel` from the committed PMC measurement, or None."""
+def measured_traffic(kernel, fetch_scale=2.0):
+    """Mean HBM bytes per launch of `kernel` from the committed PMC measurement, or None.
+    fetch_scale: the gfx950 FETCH_SIZE correction (x2 for coalesced 16-B-per-lane reads and
+    LDS-DMA, the committed figure; x1.5 for isolated 64-B segment reads, reported beside it)."""
     try:
         with open(TRAFFIC_FILE) as f:
-            return json.load(f)["kernels"][kernel]["traffic_bytes_per_launch"]
+            k = json.load(f)["kernels"][kernel]
     except (OSError, KeyError, ValueError):
         return None
+    if fetch_scale == 2.0:
+        return k["traffic_bytes_per_launch"]
+    return int(k["fetch_bytes_per_launch"] * fetch_scale / 2.0) + k["write_bytes_per_launch"]
 
 
 def wmsa_work(model, batch):
@@ -421,6 +426,7 @@ def main():
                        "timed region" % timed_steps)
         if traffic is not None:
             r["algorithmic_bytes_per_launch"] = work["fwd_bytes"] // n_launch
+            r["traffic_fetch_x1_5"] = measured_traffic("wmsa_fwd", 1.5)
             r["traffic_source"] = TRAFFIC_SOURCE
         if launches:
             r["stages"] = stage_breakdown(model.module, args.batch, launches[0], 8, False)
@@ -430,6 +436,8 @@ def main():
             measured_traffic("wmsa_bwd") if default_cfg else None, work["bwd_exp"] if large else None)
         if launches:
             result["roofline_bwd"]["stages"] = stage_breakdown(model.module, args.batch, launches[1], 16, True)
+        if default_cfg and measured_traffic("wmsa_bwd") is not None:
+            result["roofline_bwd"]["traffic_fetch_x1_5"] = measured_traffic("wmsa_bwd", 1.5)
         if not large:
             # SURVEY.md §8(d) counts 16 T C backward bytes, an O read included; the w <= 8 backward
             # recomputes delta = rowsum(P dP) and never reads O, so the bytes it must move are

@@ -2,7 +2,7 @@
 # W-MSA PMC traffic passes (each GPU step under its own time limit; stops at the first failure)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/final
+O=gpurun_out/${FINAL_OUT:-final}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
