@@ -36,7 +36,7 @@ SIGNATURES = {
     "hvk_wmsa_fwd_normed": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p]),
     "hvk_wmsa_bwd_normed": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _i, _i, _i, _i, _i, _i, _i,
                                  _p]),
-    "hvk_qk_normalize": (_i, [_p, _p, _i, _i, _p]),
+    "hvk_qk_normalize": (_i, [_p, _p, _p, _i, _i, _p]),
     "hvk_linear_supported": (_i, [_i, _i, _i]),
     "hvk_linear_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_cpb_fwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p]),
@@ -44,8 +44,8 @@ SIGNATURES = {
     "hvk_cpb_bwd": (_i, [_p, _p, _p, _p, _p, _f, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _sz,
                          _p]),
     "hvk_linear_qkv_supported": (_i, [_i, _i, _i]),
-    "hvk_linear_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
-    "hvk_gemm_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_linear_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
+    "hvk_gemm_qkv_fwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_linear_gelu_supported": (_i, [_i, _i, _i]),
     "hvk_linear_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_supported": (_i, [_i, _i, _i]),
@@ -70,6 +70,7 @@ SIGNATURES = {
                            _p]),
     "hvk_weight_grad_workspace": (_sz, [_i, _i, _i]),
     "hvk_weight_grad": (_i, [_p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
+    "hvk_weight_grad_shift": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
     "hvk_mlp_fwd_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),

@@ -29,8 +29,8 @@ __device__ __forceinline__ void attn_bias_fwd_body(int bid, int nblk, const floa
   }
 }
 
-// kAbRows rows n of W per workgroup: d W[n, :] = g[n] v^T and the rows' share of d v = W^T g
-// (column partial sums, one f32 atomic per column per workgroup into d v, zeroed forward)
+// kAbRows rows n of W per workgroup: d W[n, :] = g[n] v^T (dw not null) and the rows' share of
+// d v = W^T g (column partial sums, one f32 atomic per column per workgroup into d v, zeroed forward)
 __device__ __forceinline__ void attn_bias_bwd_body(int bid, const float* __restrict__ g,
                                                    const float* __restrict__ vb, const float* __restrict__ w,
                                                    int C, float* __restrict__ dpb, float* __restrict__ dvb,
@@ -44,7 +44,7 @@ __device__ __forceinline__ void attn_bias_bwd_body(int bid, const float* __restr
       const int n = n0 + r;
       if (n < C) {
         const float gn = g[n];
-        dw[(size_t)n * C + k] = gn * vk;
+        if (dw) dw[(size_t)n * C + k] = gn * vk;  // null: the proj weight-gradient kernel adds it
         acc = fmaf(w[(size_t)n * C + k], gn, acc);
       }
     }

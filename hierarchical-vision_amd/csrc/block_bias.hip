@@ -85,8 +85,8 @@ int hvk_block_bias_bwd(const float* g_eff, const float* v_bias, const float* pro
   if (!v_bias || !proj_w || !coords || !w1 || !b1 || !w2 || !logit_scale || !table || !dtable || !dscale ||
       !dw1 || !db1 || !dw2 || !dlogit || !workspace || C <= 0)
     return hvk_set_error(HVK_EINVAL, "hvk_block_bias_bwd: null pointer or C=%d", C);
-  if (g_eff && (!d_v_bias || !d_proj_w))
-    return hvk_set_error(HVK_EINVAL, "hvk_block_bias_bwd: null attention-bias gradient output");
+  if (g_eff && !d_v_bias)
+    return hvk_set_error(HVK_EINVAL, "hvk_block_bias_bwd: null d v_bias");
   if (hidden != kHid || nH <= 0 || nH > 32 || RR <= 0)
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_block_bias_bwd: hidden=%d (512) nH=%d (<= 32)", hidden, nH);
   const int nblk = (RR + kRowsPerBlock - 1) / kRowsPerBlock;

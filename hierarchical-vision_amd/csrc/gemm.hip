@@ -59,7 +59,8 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
                                                           hvk_bf16* __restrict__ Y,
                                                           hvk_bf16* __restrict__ Y2, int M, int N,
                                                           int ncb, int row_groups,
-                                                          float* __restrict__ csum = nullptr) {
+                                                          float* __restrict__ csum = nullptr,
+                                                          const float* __restrict__ qscale = nullptr) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -192,8 +193,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
         if constexpr (EPI == 4) {
           const int qk_cols = 2 * (N / 3), col = n0 + 32 * j;
           if (col < qk_cols) {  // wave-uniform: the v column blocks skip it
+            // q slices (col < N/3) as q^ * scale_h * log2e (tile_epilogue, gemm_tile.hip)
+            const float post = (qscale && col < N / 3) ? qscale[col / 32] * HVK_LOG2E : 1.f;
             float r;
-            hv = hvk_head_normalize8(hv, r);  // all 64 lanes take part in the group sums
+            hv = hvk_head_normalize8(hv, r, post);  // all 64 lanes take part in the group sums
             rq[j] = r;
           }
         }
@@ -490,7 +493,8 @@ int g_cu_count = 0;
 
 template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
 int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
-                  int N, hipStream_t st, hvk_bf16* Y2 = nullptr, float* csum = nullptr) {
+                  int N, hipStream_t st, hvk_bf16* Y2 = nullptr, float* csum = nullptr,
+                  const float* qscale = nullptr) {
   using G = GCfg<K, BN>;
   constexpr int kThreads = 64 * WAVES;
   auto kb = &linear_kernel<K, BN, WAVES, PREF, true, EPI>;
@@ -525,10 +529,10 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   const double flops = 2.0 * M * N * K;
   if (bias)
     HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
-                       ncb, row_groups, csum);
+                       ncb, row_groups, csum, qscale);
   else
     HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
-                       ncb, row_groups, csum);
+                       ncb, row_groups, csum, qscale);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }
@@ -607,8 +611,8 @@ int hvk_linear_qkv_supported(int M, int K, int N) {
           (K == 256 && c->BN == 128)) && c->waves == 8 && c->pref == 1;
 }
 
-int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K, int N,
-                       void* stream) {
+int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, const float* qscale,
+                       int M, int K, int N, void* stream) {
   if (!x || !w || !y || !rn) return hvk_set_error(HVK_EINVAL, "hvk_linear_qkv_fwd: null pointer");
   if (!hvk_linear_qkv_supported(M, K, N))
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_qkv_fwd: shape M=%d K=%d N=%d not built", M, K, N);
@@ -616,10 +620,10 @@ int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y,
   const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
   const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
   hvk_bf16* Y = static_cast<hvk_bf16*>(y);
-  if (K == 96) return launch_linear<96, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
-  if (K == 192) return launch_linear<192, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
-  if (K == 128) return launch_linear<128, 192, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
-  return launch_linear<256, 128, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn);
+  if (K == 96) return launch_linear<96, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn, qscale);
+  if (K == 192) return launch_linear<192, 288, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn, qscale);
+  if (K == 128) return launch_linear<128, 192, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn, qscale);
+  return launch_linear<256, 128, 8, true, 4>(X, W, bias, Y, M, N, st, nullptr, rn, qscale);
 }
 
 int hvk_linear_gelu_supported(int M, int K, int N) {

@@ -100,7 +100,8 @@ template <int EPI, int NT, int MT, int HPRE = 0>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
                                               int N, int row0, int col0,
-                                              const uint4 (*hpre)[NT / 2] = nullptr, float* __restrict__ rn = nullptr) {
+                                              const uint4 (*hpre)[NT / 2] = nullptr, float* __restrict__ rn = nullptr,
+                                              const float* __restrict__ qscale = nullptr) {
   // HPRE: h of token tiles 0 .. HPRE-1 was loaded early by the caller (hpre)
   const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   float bv[NT / 2][8];
@@ -124,6 +125,16 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
   hvk_u32x4 pk[MT][NT / 2], pg[EPI == 1 ? MT : 1][NT / 2];
   float rv[EPI == 4 ? MT : 1][NT / 2];
   const int qk_cols = 2 * (N / 3);
+  // EPI 4: q slices (columns < N/3) come out as q^ * scale_h * log2e (qscale = the head's
+  // exp(clamp(logit_scale)), the W-MSA forward's logit scale), k slices as k^
+  float qpost[EPI == 4 ? NT / 2 : 1];
+  if constexpr (EPI == 4) {
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j) {
+      const int c = col0 + 32 * j;
+      qpost[j] = (qscale && c < N / 3) ? qscale[c / 32] * HVK_LOG2E : 1.f;
+    }
+  }
 #pragma unroll
   for (int b = 0; b < MT; ++b)
 #pragma unroll
@@ -155,7 +166,7 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
         rv[b][j] = 0.f;
         if (col0 + 32 * j < qk_cols) {  // wave-uniform: the v column blocks skip it
           float r;
-          pk[b][j] = __builtin_bit_cast(hvk_u32x4, hvk_head_normalize8(hv, r));  // all 64 lanes
+          pk[b][j] = __builtin_bit_cast(hvk_u32x4, hvk_head_normalize8(hv, r, qpost[j]));  // all 64 lanes
           rv[b][j] = r;
         }
       }
@@ -200,7 +211,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
                                                         const float* __restrict__ bias,
                                                         hvk_bf16* __restrict__ Y,
                                                         hvk_bf16* __restrict__ Y2, int M, int N,
-                                                        int K, int mtiles, float* __restrict__ rn) {
+                                                        int K, int mtiles, float* __restrict__ rn,
+                                                        const float* __restrict__ qscale) {
   using T = TileCfg<TN>;
   constexpr int BN = T::BN, STAGE_BYTES = T::STAGE, TILE_BYTES = T::WTILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -342,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn);
+  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn, qscale);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
@@ -573,7 +585,7 @@ int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16*
 
 template <int EPI, bool PIPE, int TN>
 int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                 int M, int N, int K, hipStream_t st, float* rn = nullptr) {
+                 int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr) {
   using T = TileCfg<TN>;
   static bool attr = false;
   if (!attr) {
@@ -585,7 +597,7 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / T::BN));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
-                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn);
+                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }
@@ -593,15 +605,15 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
 // 128 x 128 or 128 x 192 tiles
 template <int EPI>
 int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                int M, int N, int K, hipStream_t st, float* rn = nullptr) {
+                int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr) {
   // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1536 case
   // (tools/bench_gemm.py, interleaved: 3-25 % faster on the stage-2/3 shapes, 6 % slower on
   // the stage-2 projection); option "tile_wide" 0 / 1 forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
   if constexpr (EPI == 4) {  // the qkv form: the 128-row tile kernel only
     if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536)))
-      return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn);
-    return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn);
+      return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
+    return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
   } else {
   {
     const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
@@ -666,13 +678,13 @@ int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, in
                         static_cast<hipStream_t>(stream));
 }
 
-int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
+int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, const float* qscale, int M, int K,
                      int N, void* stream) {
   if (!x || !w || !y || !rn) return hvk_set_error(HVK_EINVAL, "hvk_gemm_qkv_fwd: null pointer");
   if (!hvk_gemm_supported(M, K, N) || N % 96)
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_qkv_fwd: M=%d K=%d N=%d (N = 3C, 32 | C)", M, K, N);
   return launch_tile<4>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
-                        static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream), rn);
+                        static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream), rn, qscale);
 }
 
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M, int K,

@@ -210,30 +210,47 @@ __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN 
   }
 }
 
-// dW / db = sum over the chunks' slabs; 32 float4 columns x 8 chunk phases per workgroup
+// dW / db = sum over the chunks' slabs; 32 float4 columns x 8 chunk phases per workgroup.
+// xshift (K floats) or null: dW += db (x) xshift, i.e. dW = g^T (x + 1 xshift^T) -- the proj
+// Linear's input is o + v_bias in the reference (swinv2.py:255-262) while the GEMM ran on o, its
+// v_bias share folded into the bias (hvk_block_bias_fwd); db[n] is re-summed from the slabs here
+// (K / 4 threads share each row's partials through L2).  db null: not stored.
 __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict__ P, int e4,
                                                         int ndw4, int nchunk, long pstride4,
                                                         float4* __restrict__ dw,
-                                                        float4* __restrict__ db) {
+                                                        float4* __restrict__ db,
+                                                        const float* __restrict__ xshift, int K) {
   __shared__ float4 red[8][32];
+  __shared__ float redd[8][32];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int e = blockIdx.x * 32 + tx;
+  const int n = (4 * e) / K;  // the dW row of this float4 (e < ndw4)
+  const float* Pdb = reinterpret_cast<const float*>(P) + 4 * (size_t)ndw4 + n;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  float sd = 0.f;
   if (e < e4) {
 #pragma unroll 4
     for (int c = ty; c < nchunk; c += 8) {
       const float4 v = P[(size_t)c * pstride4 + e];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      if (xshift && e < ndw4) sd += Pdb[(size_t)c * pstride4 * 4];
     }
   }
   red[ty][tx] = s;
+  redd[ty][tx] = sd;
   __syncthreads();
   if (ty == 0 && e < e4) {
 #pragma unroll
     for (int j = 1; j < 8; ++j) {
       const float4 v = red[j][tx];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      sd += redd[j][tx];
     }
+    if (xshift && e < ndw4) {
+      const float4 xs = *reinterpret_cast<const float4*>(xshift + (4 * e) % K);
+      s.x = fmaf(sd, xs.x, s.x); s.y = fmaf(sd, xs.y, s.y); s.z = fmaf(sd, xs.z, s.z); s.w = fmaf(sd, xs.w, s.w);
+    }
+    if (e >= ndw4 && !db) return;
     float4* dst = e < ndw4 ? dw + e : db + (e - ndw4);
     if (HVK_NT_SAVED & 64)  // read only by the optimizer at the end of the step
       hvk_st16_nt(dst, make_uint4(__float_as_uint(s.x), __float_as_uint(s.y), __float_as_uint(s.z),
@@ -247,7 +264,9 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict
 // or 192 x 384 tile for the rest; default 192 x 192 on 8 waves (tools/bench_dw.py: fastest
 // with the fused bias gradient on every stage 1-3 shape); B256 / B128: 128 x 256 and 128 x 128
 // tiles for the widths 192 does not divide (SwinV2-B: C = 128 ... 1024)
-enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C, V_B256, V_B128 };
+// V_T4 .. V_T8C are the option "dw_tile" values 4 .. 8 (tile_variant): keep their numbers
+enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C, V_B256, V_B128, V_96x48 };
+static_assert(V_T4 == 4 && V_T8C == 8, "dw_tile option values");
 
 struct Plan {
   int var = -1, tk = 0, tn = 0, ntk = 0, ntiles = 0, nslices = 0, nchunk = 0;
@@ -264,6 +283,7 @@ bool plan(int M, int N, int K, Plan& p) {
   else if (N == 96 && K == 96) p.var = V_96x96, p.tk = 96, p.tn = 96;
   else if (N == 384 && K == 96) p.var = V_384x96, p.tk = 96, p.tn = 384;
   else if (N == 96 && K == 384) p.var = V_96x384, p.tk = 384, p.tn = 96;
+  else if (N == 96 && K == 48) p.var = V_96x48, p.tk = 48, p.tn = 96;  // the patch embedding (4x4x3 -> 96)
   else if (N % 192 == 0 && K % 192 == 0 && N <= 8192 && K <= 8192) {
     p.var = tile_variant();
     if (p.var < V_T4 || p.var > V_T8C || (p.var == V_T8W && N % 384)) p.var = V_T4;
@@ -328,7 +348,7 @@ size_t hvk_weight_grad_workspace(int M, int N, int K) {
 }
 
 static int weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
-                       size_t ws_bytes, void* stream, bool gx) {
+                       size_t ws_bytes, void* stream, bool gx, const float* xshift = nullptr) {
   if (!g || !x || !dw || !ws) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad: null pointer");
   Plan p;
   if (!plan(M, N, K, p))
@@ -339,7 +359,7 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
   const hvk_bf16* gb = static_cast<const hvk_bf16*>(g);
   const hvk_bf16* xb = static_cast<const hvk_bf16*>(x);
   float* P = static_cast<float*>(ws);
-  const bool wd = db != nullptr;
+  const bool wd = db != nullptr || xshift != nullptr;  // the shift needs the bias partials
   int rc;
   if (gx && p.var != V_96x384)
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_weight_grad_gelu_x: M=%d N=%d K=%d", M, N, K);
@@ -347,6 +367,7 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
     case -1: rc = launch<12, 3, 2, 2, true>(gb, xb, P, wd, N, K, p, st); break;
     case V_288x96: rc = launch<3, 9, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x96: rc = launch<3, 3, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
+    case V_96x48: rc = launch<3, 3, 1, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_384x96: rc = launch<3, 12, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x384: rc = launch<12, 3, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_T8A: rc = launch<6, 3, 2, 4>(gb, xb, P, wd, N, K, p, st); break;
@@ -362,7 +383,7 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
   const int e4 = wd ? (int)(p.pstride / 4) : ndw4;
   hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((e4 + 31) / 32)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(P), e4, ndw4, p.nchunk, p.pstride / 4,
-                     reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db));
+                     reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db), xshift, K);
   HVK_CHECK_LAUNCH("hvk_weight_grad_reduce");
   return HVK_OK;
 }
@@ -370,6 +391,12 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
 int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
                     size_t ws_bytes, void* stream) {
   return weight_grad(g, x, dw, db, M, N, K, ws, ws_bytes, stream, false);
+}
+
+int hvk_weight_grad_shift(const void* g, const void* x, const float* xshift, float* dw, float* db, int M, int N,
+                          int K, void* ws, size_t ws_bytes, void* stream) {
+  if (!xshift) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad_shift: null xshift");
+  return weight_grad(g, x, dw, db, M, N, K, ws, ws_bytes, stream, false, xshift);
 }
 
 int hvk_weight_grad_gelu_x_supported(int M, int N, int K) {

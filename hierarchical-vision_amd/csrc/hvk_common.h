@@ -369,7 +369,7 @@ __device__ __forceinline__ float hvk_group4_max(float v) { return hvk_xor32_max(
 // Returns the normalised bf16 values and rn = 1 / max(||x||, 1e-12) -- the arithmetic of
 // wmsa_common.h's l2_normalize (dot2 sum of squares, group-4 sum, rsq), which the w <= 8
 // attention kernels ran on the loaded rows before round 4.
-__device__ __forceinline__ uint4 hvk_head_normalize8(uint4 v, float& rn) {
+__device__ __forceinline__ uint4 hvk_head_normalize8(uint4 v, float& rn, float post = 1.f) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
   auto d2 = [](uint32_t w, float c) {
     return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, w), __builtin_bit_cast(bf16x2_t, w), c, false);
@@ -379,14 +379,7 @@ __device__ __forceinline__ uint4 hvk_head_normalize8(uint4 v, float& rn) {
   hvk_unpack8(v, f);
   ss = hvk_group4_sum(ss);
   rn = __builtin_amdgcn_rsqf(fmaxf(ss, 1e-24f));
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] *= rn;
-  return hvk_pack8(f);
-}
-// 8 packed bf16 times a scalar, rounded back to bf16
-__device__ __forceinline__ uint4 hvk_scale8(uint4 v, float m) {
-  float f[8];
-  hvk_unpack8(v, f);
+  const float m = rn * post;  // post: the q slices' scale * log2e (wmsa_common.h's l2_normalize)
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] *= m;
   return hvk_pack8(f);

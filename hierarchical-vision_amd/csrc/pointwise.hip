@@ -110,7 +110,7 @@ namespace {
 // head (lane = row li, 8-channel chunk g), the layout of the fused GEMM epilogues, so the sums
 // of squares reduce in the same order and the results are bit-identical to theirs
 __global__ __launch_bounds__(256) void qk_normalize_kernel(hvk_bf16* __restrict__ qkv, float* __restrict__ rn,
-                                                           int T, int C) {
+                                                           const float* __restrict__ qscale, int T, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int heads2 = 2 * C / 32;
@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) void qk_normalize_kernel(hvk_bf16* __restrict_
   const size_t off = (size_t)(ok ? row : 0) * 3 * C + hd * 32 + 8 * g;
   uint4 v = *reinterpret_cast<const uint4*>(qkv + off);
   float r;
-  v = hvk_head_normalize8(v, r);  // all 64 lanes take part in the group sums
+  const float post = (qscale && hd < C / 32) ? qscale[hd] * HVK_LOG2E : 1.f;  // q: q^ * scale * log2e
+  v = hvk_head_normalize8(v, r, post);  // all 64 lanes take part in the group sums
   if (ok) {
     *reinterpret_cast<uint4*>(qkv + off) = v;
     if (g == 0) rn[(size_t)row * heads2 + hd] = r;
@@ -133,14 +134,14 @@ __global__ __launch_bounds__(256) void qk_normalize_kernel(hvk_bf16* __restrict_
 
 extern "C" {
 
-int hvk_qk_normalize(void* qkv, float* rn, int T, int C, void* stream) {
+int hvk_qk_normalize(void* qkv, float* rn, const float* qscale, int T, int C, void* stream) {
   if (!qkv || !rn) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: null pointer");
   if (T <= 0 || C <= 0 || C % 32) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: T=%d C=%d (C %% 32)", T, C);
   const long long items = (long long)((T + 15) / 16) * (2 * C / 32);
   const long long grid = (items + 3) / 4;
   if (grid > 0x7fffffffLL) return hvk_set_error(HVK_EINVAL, "hvk_qk_normalize: too many rows");
   hipLaunchKernelGGL(qk_normalize_kernel, dim3((unsigned)grid), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<hvk_bf16*>(qkv), rn, T, C);
+                     static_cast<hvk_bf16*>(qkv), rn, qscale, T, C);
   HVK_CHECK_LAUNCH("hvk_qk_normalize");
   return HVK_OK;
 }

@@ -220,6 +220,8 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   for (int e = threadIdx.x; e < 2 * PC::PAIR_LDS; e += kThreads) img0[e] = 0;
   const float scale = a.scale[h];
   const float sc2 = scale * HVK_LOG2E;
+  // uniform: kept in an SGPR (readfirstlane), not a VGPR of this 256-VGPR kernel
+  const float inv_sc2 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(1.f / sc2)));
   build_bounded_table<WIN>(btab, btab + K::TAB, a.bias + (size_t)h * K::R * K::R, sc2);
 
   const int li = lane & 15, gq = lane >> 4;
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
           const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = fmaf(s[ki][r], sc2, bv[r]);
+            float x = NORMED ? s[ki][r] + bv[r] : fmaf(s[ki][r], sc2, bv[r]);  // NORMED: s = q^ sc2 . k^
             if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
             p[ki][r] = __builtin_amdgcn_exp2f(x);
             sum += p[ki][r];
@@ -404,7 +406,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
             const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float x = fmaf(s[ki][r], sc2, bv[r]);
+              float x = NORMED ? s[ki][r] + bv[r] : fmaf(s[ki][r], sc2, bv[r]);  // NORMED: s = q^ sc2 . k^
               if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
               p[ki][r] = x;
               mx = fmaxf(mx, x);
@@ -466,6 +468,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
           for (int r = 0; r < 4; ++r) dot += qh[dt][r] * dq[dt][r];
         }
         dot = hvk_group4_sum(dot);
+        if constexpr (NORMED) dot *= inv_sc2 * inv_sc2;  // qh = q^ sc2: q^ (q^ . dq^) = qh (qh . dq^) / sc2^2
         if (rnq[j] >= 1e12f) dot = 0.f;  // ||q|| <= eps: x / eps, no projection term
         uint2 pk[2];
 #pragma unroll
@@ -527,12 +530,15 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
         }
         dot = hvk_group4_sum(dot);
         if (rnk[j] >= 1e12f) dot = 0.f;
+        // NORMED: the q^ image holds q^ sc2, so dk here is sc2 dK^ (linear: the projection term
+        // scales with it); one factor on the row's 1/||k||
+        const float rk = NORMED ? rnk[j] * inv_sc2 : rnk[j];
         uint2 pk[2], pv[2];
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rnk[j];
+          for (int r = 0; r < 4; ++r) v[r] = (dk[dt][r] - kh[dt][r] * dot) * rk;
           pk[dt] = make_uint2(hvk_pack2(v[0], v[1]), hvk_pack2(v[2], v[3]));
           pv[dt] = make_uint2(hvk_pack2(dv[dt][0], dv[dt][1]), hvk_pack2(dv[dt][2], dv[dt][3]));
         }
@@ -578,7 +584,8 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
     atomicAdd(dst + e, (red0[e] + red0[PC::PAIR_LDS / 2 + e]) * inv_scale);
 #endif
   dscale = hvk_wave_sum(dscale);
-  if (lane == 0) atomicAdd(a.dscale_acc + h, dscale * inv_scale);
+  // NORMED: the products summed were dS (sc2 cos)
+  if (lane == 0) atomicAdd(a.dscale_acc + h, NORMED ? dscale * inv_scale * inv_sc2 : dscale * inv_scale);
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll

@@ -165,7 +165,7 @@ struct FwdArgs {
   WmsaGeom g;
   FastDiv fd_groups, fd_img, fd_ww;  // wmsa_win.hip: / (nH / HG), / (nWh nWw), / nWw
   int dma_nt;                         // wmsa_win.hip: slab DMA with the nontemporal hint
-  int qk_normed;             // 1: q and k head slices arrive L2-normalised (the qkv GEMM's EPI 4)
+  int qk_normed;             // 1: q^ * scale * log2e and k^ arrive from the qkv GEMM's EPI 4
 };
 
 struct BwdArgs {
@@ -182,7 +182,7 @@ struct BwdArgs {
   float* dscale_acc;         // [nH]
   float* dqb_acc;            // [C]   column sums of dq (q_bias gradient)
   const float* rn;           // [T, 2nH] 1/max(||q||, eps), 1/max(||k||, eps) when q and k arrive
-                             // normalised (windows <= 8), null for raw q and k
+                             // normalised, q as q^ * scale * log2e (windows <= 8); null: raw q, k
   WmsaGeom g;
 };
 

@@ -471,7 +471,8 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
 // phase 2's q / dO rows, phase 2 the next window's k / v rows) and written to LDS between the
 // phases; every tile's own global inputs are loaded one tile ahead.  Interior windows and
 // unshifted blocks run mask-free copies of both loops.
-#ifndef HVK_LARGE_PROBE  // tools/ timing probes of the backward's phase 2 (results wrong)
+#ifndef HVK_LARGE_PROBE  // tools/ timing probes of the backward (results wrong): 1 no CPB bins, 2 no
+                         // row-constant reads, 3 phase 1 skipped, 4 phase 2 skipped
 #define HVK_LARGE_PROBE 0
 #endif
 
@@ -704,7 +705,11 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     // tile wait for the row prefetch (issued next, consumed after the phase)
     QIn cur = load_qt(wave);
     load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
+#if HVK_LARGE_PROBE == 3  // probe: phase 1 skipped (timing only)
+    for (int qt = K::NT; qt < K::NT; qt += F::WAVES) {
+#else
     for (int qt = wave; qt < K::NT; qt += F::WAVES) {
+#endif
       QIn nxt = cur;
       if (qt + F::WAVES < K::NT) nxt = load_qt(qt + F::WAVES);
       const int pos = 16 * qt + li;
@@ -877,7 +882,11 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     };
     KIn kc = load_kt(wave);
     if (w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
+#if HVK_LARGE_PROBE == 4  // probe: phase 2 skipped (timing only)
+    for (int kt = K::NT; kt < K::NT; kt += F::WAVES) {
+#else
     for (int kt = wave; kt < K::NT; kt += F::WAVES) {
+#endif
       KIn kn = kc;
       if (kt + F::WAVES < K::NT) kn = load_kt(kt + F::WAVES);
       const int pos = kt + K::NT * li;

@@ -286,10 +286,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_ring_kernel(FwdArgs a) {
     continue;
 #endif
     float rn;
-    if (a.qk_normed) {  // q^ and k^ from the qkv GEMM's epilogue
-#pragma unroll
-      for (int i = 0; i < K::NT; ++i) qf[i] = hvk_scale8(qf[i], sc2);
-    } else {
+    if (!a.qk_normed) {  // qk_normed: q^ * scale * log2e and k^ arrive from the qkv GEMM's epilogue
 #pragma unroll
       for (int i = 0; i < K::NT; ++i) {
         qf[i] = l2_normalize(qf[i], rn, sc2);  // q^ * scale * log2e: the MFMA applies the scale

@@ -311,10 +311,7 @@ __global__ __launch_bounds__(64 * HG, 4) void wmsa_fwd_win_kernel(FwdArgs a) {
   static_assert(MM != 1 || (WIN == 7 && K::PW == 8), "the tile-uniform mask form is w7 / shift 3 only");
   const float colmask = (edge_c && (((li >> 2) ^ gq) & 1)) ? mask2 : 0.f;  // query x >= 4 vs key x >= 4
   float rn;
-  if (a.qk_normed) {  // q^ and k^ from the qkv GEMM's epilogue: only the logit scale left
-#pragma unroll
-    for (int i = 0; i < K::NT; ++i) qf[i] = hvk_scale8(qf[i], sc2);
-  } else {
+  if (!a.qk_normed) {  // qk_normed: q^ * scale * log2e and k^ arrive from the qkv GEMM's epilogue
 #pragma unroll
     for (int i = 0; i < K::NT; ++i) {
       qf[i] = l2_normalize(qf[i], rn, sc2);

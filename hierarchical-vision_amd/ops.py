@@ -156,13 +156,14 @@ def _gelu_recompute(M, K, N1, N2):
             and lib.hvk_weight_grad_gelu_x_supported(M, N2, N1))
 
 
-def weight_grad(g, x, with_db=False, gelu_x=False):
+def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None):
     """(dW, db) = (g^T x, g.sum(0)) in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to
     ~10^6): libhvk's token-chunked MFMA kernel with the bias gradient fused (hvk_weight_grad,
     one pass over g) for every SwinV2-T shape it is built for; otherwise the library GEMM
     batched over token chunks (thousands of workgroups) + a small sum.  db is None unless
     with_db.  gelu_x: x holds the fc1 pre-activation h and the kernel contracts with GELU(h)
-    (hvk_weight_grad_gelu_x)."""
+    (hvk_weight_grad_gelu_x).  xshift (f32 [K]) or None: dW = g^T (x + 1 xshift^T)
+    (hvk_weight_grad_shift; the proj Linear's folded v_bias)."""
     M, N = g.shape
     K = x.shape[1]
     lib = _lib.load()
@@ -179,9 +180,17 @@ def weight_grad(g, x, with_db=False, gelu_x=False):
         db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
         nb = lib.hvk_weight_grad_workspace(M, N, K)
         ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
-        call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
-             ptr(ws), nb, stream())
+        if xshift is not None:
+            call("hvk_weight_grad_shift", ptr(g), ptr(x), ptr(_f32(xshift)), ptr(dw), ptr(db) if with_db else None,
+                 M, N, K, ptr(ws), nb, stream())
+        else:
+            call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
+                 ptr(ws), nb, stream())
         return dw, db
+    if xshift is not None:
+        dw, db = weight_grad(g, x, True)
+        dw.add_(torch.outer(db, _f32(xshift)))
+        return dw, (db if with_db else None)
     db = g.sum(dim=0, dtype=torch.float32) if with_db else None
     nc = _split_k_chunks(M)
     if nc == 1:
@@ -286,7 +295,7 @@ class LinearFn(torch.autograd.Function):
     gradient run on libhvk's skinny MFMA GEMM for the memory-bound shapes."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, xshift=None):
         xb = _bf16(x)
         wb, wt = _bf16_weight(weight)
         N, K = wb.shape
@@ -294,6 +303,7 @@ class LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.wt = wt
         ctx.has_bias = bias is not None
+        ctx.xshift = xshift.detach() if xshift is not None else None
         return y
 
     @staticmethod
@@ -308,50 +318,55 @@ class LinearFn(torch.autograd.Function):
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = None, None
         if ctx.needs_input_grad[1]:
-            dw, db = weight_grad(g2, xb.reshape(-1, K), want_db)
+            dw, db = weight_grad(g2, xb.reshape(-1, K), want_db, xshift=getattr(ctx, "xshift", None))
         elif want_db:
             db = g2.sum(dim=0, dtype=torch.float32)
-        return gx, dw, db
+        return gx, dw, db, None
 
 
-def linear(x, weight, bias=None):
-    return LinearFn.apply(x, weight, bias)
+def linear(x, weight, bias=None, xshift=None):
+    """F.linear on libhvk's GEMMs.  xshift (detached, [K]) or None: the weight gradient is taken
+    for the input x + xshift (the proj Linear, whose v_bias share of the input was folded into
+    its bias by block_tables: swinv2.py:255-262)."""
+    return LinearFn.apply(x, weight, bias, xshift)
 
 
-def qkv_nt(x2, wb, bias):
+def qkv_nt(x2, wb, bias, scale):
     """(qkv^, rn) for the qkv Linear of a w <= 8 block: y = x2 wb^T + bias with every q and k
-    head slice L2-normalised (the F.normalize of swinv2.py:229) and rn [M, 2N/96] = their
-    1 / max(||x||, eps), in the GEMM's epilogue where it is built (hvk_linear_qkv_fwd /
-    hvk_gemm_qkv_fwd), else mm_nt + hvk_qk_normalize in place."""
+    head slice L2-normalised (the F.normalize of swinv2.py:229), q times scale[h] * log2e (the
+    attention's logit scale, `scale` f32 [nH]), and rn [M, 2N/96] = their 1 / max(||x||, eps),
+    in the GEMM's epilogue where it is built (hvk_linear_qkv_fwd / hvk_gemm_qkv_fwd), else
+    mm_nt + hvk_qk_normalize in place."""
     M, K = x2.shape
     N = wb.shape[0]
     lib = _lib.load()
     y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
     rn = torch.empty((M, 2 * N // 96), device=x2.device, dtype=torch.float32)
     b = ptr(_f32(bias)) if bias is not None else None
+    sc = _f32(scale.detach())  # its gradient comes from the attention core (logit = scale cos)
     if _tile_ok(M, K, N) and not _skinny_first(M, K, N) and N % 96 == 0:
-        call("hvk_gemm_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), M, K, N, stream())
+        call("hvk_gemm_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), ptr(sc), M, K, N, stream())
     elif _linear_native(M, K, N) and lib.hvk_linear_qkv_supported(M, K, N):
-        call("hvk_linear_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), M, K, N, stream())
+        call("hvk_linear_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), ptr(sc), M, K, N, stream())
     else:
         y = mm_nt(x2, wb, bias)
-        call("hvk_qk_normalize", ptr(y), ptr(rn), M, N // 3, stream())
+        call("hvk_qk_normalize", ptr(y), ptr(rn), ptr(sc), M, N // 3, stream())
     return y, rn
 
 
 class LinearQkvFn(torch.autograd.Function):
-    """The qkv Linear with the q / k normalisation of the attention that consumes it
-    (swinv2.py:220 + 229): returns (qkv^, rn), see qkv_nt.  Its only consumer,
+    """The qkv Linear with the q / k normalisation (and logit scale) of the attention that
+    consumes it (swinv2.py:220 + 229-231): returns (qkv^, rn), see qkv_nt.  Its only consumer,
     WindowAttentionCore with rn, returns the gradient with respect to the UN-normalised qkv
     (hvk_wmsa_bwd_normed applies the normalisation's backward), so the backward here is
     LinearFn's."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, scale):
         xb = _bf16(x)
         wb, wt = _bf16_weight(weight)
         N, K = wb.shape
-        y, rn = qkv_nt(xb.reshape(-1, K), wb, bias)
+        y, rn = qkv_nt(xb.reshape(-1, K), wb, bias, scale)
         ctx.save_for_backward(xb, wb)
         ctx.wt = wt
         ctx.has_bias = bias is not None
@@ -362,12 +377,14 @@ class LinearQkvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy, grn):
         if gy is None:
-            return None, None, None
-        return LinearFn.backward(ctx, gy)
+            return None, None, None, None
+        return LinearFn.backward(ctx, gy)  # (gx, dW, db, None for scale)
 
 
-def linear_qkv(x, weight, bias=None):
-    return LinearQkvFn.apply(x, weight, bias)
+def linear_qkv(x, weight, bias, scale):
+    """The qkv Linear with q, k normalised and q pre-scaled by the attention's logit scale
+    (`scale` [nH], detached here: its gradient comes from window_attention_core)."""
+    return LinearQkvFn.apply(x, weight, bias, scale)
 
 
 # --------------------------------------------------------------------------- classifier head
@@ -695,7 +712,9 @@ class BlockTables(torch.autograd.Function):
         dv, dpw, dpb = None, None, None
         if g_eff is not None:
             g_eff = _f32(g_eff)
-            dv, dpw = ctx.dv, torch.empty_like(pw)
+            # proj_w passed detached: its v_bias share is added by the proj Linear's weight-gradient
+            # kernel (linear(..., xshift=v_bias)), no separate C x C gradient and accumulation here
+            dv, dpw = ctx.dv, (torch.empty_like(pw) if ctx.needs_input_grad[2] else None)
             dpb = torch.empty_like(g_eff) if ctx.has_pb else None
         ctx.dv = None  # the returned d v_bias is then its only reference: AccumulateGrad steals it
         dtable = _f32(dtable) if dtable is not None else torch.zeros_like(table)

@@ -231,9 +231,13 @@ class WindowAttention(nn.Module):
         if (self.v_bias is not None and self.v_bias.is_cuda and _FUSED_TABLES
                 and isinstance(self.cpb_mlp[1], nn.ReLU) and l1.bias is not None and l2.bias is None
                 and l1.out_features == 512 and self.num_heads <= 32):
-            return ops.block_tables(self.v_bias, self.proj.bias, self.proj.weight,
+            # W_proj enters the folded bias detached: forward_tokens' proj Linear takes the
+            # W_proj v_bias share of its weight gradient (xshift = v_bias, one fused kernel)
+            self._proj_fold = True  # a plain bool (a Parameter attribute would register a parameter)
+            return ops.block_tables(self.v_bias, self.proj.bias, self.proj.weight.detach(),
                                     self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias,
                                     l2.weight, self.logit_scale, self.q_bias, self._logit_clamp)
+        self._proj_fold = False
         return self.gemm_biases() + self.cpb_tables()
 
     def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None):
@@ -246,12 +250,13 @@ class WindowAttention(nn.Module):
         table, scale = biases[2:] if len(biases) == 4 else self.cpb_tables()
         if _QK_EPILOGUE and self.window_size[0] <= 8:
             # q / k normalisation (swinv2.py:229) in the qkv GEMM's epilogue
-            qkv, rn = ops.linear_qkv(x, self.qkv.weight, qkv_b)
+            qkv, rn = ops.linear_qkv(x, self.qkv.weight, qkv_b, scale)
         else:
             qkv, rn = ops.linear(x, self.qkv.weight, qkv_b), None
         o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
                                       self.window_size[0], shift, q_bias=self.q_bias, rn=rn)
-        return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None))
+        return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None,
+                                         xshift=self.v_bias if getattr(self, "_proj_fold", False) else None))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""

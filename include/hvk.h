@@ -100,25 +100,26 @@ int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float
                  float* dq_bias, const float* bias_table, const float* scale, float* dbias_table,
                  float* dscale, float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
                  int num_heads, int window, int shift, void* stream);
-/* The w <= 8 pair with the q and k normalisation of swinv2.py:229 done upstream, by the qkv
- * Linear's epilogue (hvk_linear_qkv_fwd / hvk_gemm_qkv_fwd) or hvk_qk_normalize: qkv holds
- * (q^, k^, v) with q^ = F.normalize(q), k^ = F.normalize(k) per head, rounded to bf16, and
- * rn: f32 [B*H*W, 2 num_heads] = 1 / max(||q||, 1e-12) (columns 0..nH-1) and 1 / max(||k||,
- * 1e-12) (nH..2nH-1) of the un-normalised bf16 q, k.  The backward returns dqkv with respect
- * to the UN-normalised q, k (the normalisation's backward is applied with rn), so the qkv
- * Linear's backward is unchanged.  Windows 4, 6, 7, 8 only (EUNSUPPORTED otherwise).  The
- * backward's q^, k^ and rn equal what hvk_wmsa_bwd computes from raw q, k bit for bit, so
- * both give the same dqkv; the forward's q^ * scale is rounded twice (q^, then q^ * scale)
- * instead of once. */
+/* The w <= 8 pair with the q and k normalisation of swinv2.py:229 (and the forward's logit scale)
+ * done upstream, by the qkv Linear's epilogue (hvk_linear_qkv_fwd / hvk_gemm_qkv_fwd) or
+ * hvk_qk_normalize: qkv holds (q^ * scale * log2e, k^, v) per head, q^ = F.normalize(q),
+ * k^ = F.normalize(k), rounded to bf16 once (scale = the `scale` argument, exp(clamp(logit_scale)),
+ * log2e = 1/ln 2), and rn: f32 [B*H*W, 2 num_heads] = 1 / max(||q||, 1e-12) (columns 0..nH-1)
+ * and 1 / max(||k||, 1e-12) (nH..2nH-1) of the un-normalised bf16 q, k.  The forward's q and k
+ * operands are then exactly the ones hvk_wmsa_fwd forms from raw q, k (same results bit for
+ * bit); the backward returns dqkv with respect to the UN-normalised q, k (the normalisation's
+ * backward applied with rn), so the qkv Linear's backward is unchanged.  Windows 4, 6, 7, 8 only
+ * (EUNSUPPORTED otherwise). */
 int hvk_wmsa_fwd_normed(const void* qkv, void* out, const float* bias_table, const float* scale,
                         int B, int H, int W, int C, int num_heads, int window, int shift, void* stream);
 int hvk_wmsa_bwd_normed(const void* qkv, const float* rn, const void* dout, void* dqkv, float* dq_bias,
                         const float* bias_table, const float* scale, float* dbias_table, float* dscale,
                         float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
                         int num_heads, int window, int shift, void* stream);
-/* In place: every 32-wide q and k head slice of qkv [T, C3 = 3C] (columns < 2C) normalised and
+/* In place: every 32-wide q and k head slice of qkv [T, C3 = 3C] (columns < 2C) normalised, the
+ * q slices times qscale[h] * log2e (qscale: f32 [C/32] = the W-MSA `scale`, or NULL: none), and
  * rn [T, 2C/32] written, exactly as the qkv epilogues do (for a qkv produced elsewhere). */
-int hvk_qk_normalize(void* qkv, float* rn, int T, int C, void* stream);
+int hvk_qk_normalize(void* qkv, float* rn, const float* qscale, int T, int C, void* stream);
 
 /* ---- Skinny Linear (memory-bound GEMM) ------------------------------------------------
  * y[M, N] = x[M, K] w[N, K]^T (+ bias[N]), bf16 in/out, f32 accumulation: F.linear of
@@ -134,15 +135,16 @@ int hvk_linear_fwd(const void* x, const void* w, const float* bias, void* y, int
  * backward, = the reference's fc1 output) and y = GELU(h) (exact erf, bf16); replaces
  * hvk_linear_fwd + hvk_bias_gelu_fwd where hvk_linear_gelu_supported(). */
 /* The qkv Linear of a w <= 8 block (swinv2.py:220 + the F.normalize of 229): y = x w^T + bias
- * (N = 3K) with the q and k head slices normalised and rn [M, 2K/32] written (see
+ * (N = 3K) with the q and k head slices normalised -- q times qscale[h] * log2e when qscale (f32
+ * [K/32], the block's exp(clamp(logit_scale))) is not NULL -- and rn [M, 2K/32] written (see
  * hvk_wmsa_fwd_normed); the v slice is hvk_linear_fwd's bit for bit.  Built for K = 96, 128,
  * 192, 256 (hvk_linear_qkv_supported); hvk_gemm_qkv_fwd is the tiled form (N % 96 == 0,
  * hvk_gemm_supported shapes). */
 int hvk_linear_qkv_supported(int M, int K, int N);
-int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
-                       int N, void* stream);
-int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, int M, int K,
-                     int N, void* stream);
+int hvk_linear_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, const float* qscale,
+                       int M, int K, int N, void* stream);
+int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, float* rn, const float* qscale,
+                     int M, int K, int N, void* stream);
 int hvk_linear_gelu_supported(int M, int K, int N);
 int hvk_linear_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M,
                         int K, int N, void* stream);
@@ -212,6 +214,12 @@ int hvk_weight_grad_supported(int M, int N, int K);
 size_t hvk_weight_grad_workspace(int M, int N, int K);
 int hvk_weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
                     void* ws, size_t ws_bytes, void* stream);
+/* dW = g^T (x + 1 xshift^T) = g^T x + db (x) xshift, db = sum_m g (db may be NULL: not stored):
+ * the proj Linear's weight gradient when its input's constant share v_bias (swinv2.py:255-262,
+ * P (V + v_bias) = P V + v_bias) was folded into the bias instead of the GEMM operand;
+ * xshift f32 [K].  Same shapes as hvk_weight_grad. */
+int hvk_weight_grad_shift(const void* g, const void* x, const float* xshift, float* dw, float* db, int M, int N,
+                          int K, void* ws, size_t ws_bytes, void* stream);
 /* The same with x = GELU(h) recomputed from the saved bf16 fc1 pre-activation h (bit-identical
  * to the stored GELU(h) of hvk_linear_gelu_fwd): fc2's weight gradient without GELU(h) kept
  * in HBM.  Built for the stage-0 fc2 shape (N = 96, K = 384). */
@@ -298,6 +306,8 @@ int hvk_block_bias_fwd(const float* q_bias, const float* v_bias, const float* pr
                        int C, const float* coords, const float* w1, const float* b1, const float* w2,
                        const float* logit_scale, float clamp_max, int RR, int nH, int hidden, float* qkv_bias,
                        float* eff, float* dv_zero, float* table, float* scale, void* stream);
+/* d_proj_w may be NULL: the W_proj v_bias share of the proj weight gradient is then left to the
+ * proj Linear's weight-gradient kernel (hvk_weight_grad_shift with xshift = v_bias). */
 int hvk_block_bias_bwd(const float* g_eff, const float* v_bias, const float* proj_w, int C, float* d_proj_bias,
                        float* d_v_bias, float* d_proj_w, const float* coords, const float* w1, const float* b1,
                        const float* w2, const float* logit_scale, float clamp_max, int RR, int nH, int hidden,

@@ -125,9 +125,32 @@ def test_block_tables_match_separate_launches(dim, heads, win):
     (ra, ga), (rb, gb) = outs[True], outs[False]
     for a, b in zip(ra, rb):
         assert torch.equal(a, b)
-    assert ga.keys() == gb.keys() and len(ga) >= 7, sorted(ga)
+    # the fused tables take W_proj detached: the W_proj v_bias share of its gradient is the proj
+    # Linear's (ops.linear(..., xshift=v_bias), test_proj_linear_xshift_gradient)
+    assert "proj.weight" not in ga and set(ga) | {"proj.weight"} == set(gb) and len(ga) >= 6, sorted(ga)
     for n in ga:
         assert torch.allclose(ga[n], gb[n], rtol=1e-4, atol=1e-5), n  # d v_bias: f32 atomics
+    assert m._proj_fold
+
+
+@pytest.mark.parametrize("dim,T", [(96, 6272), (384, 1568), (768, 2048)])
+def test_proj_linear_xshift_gradient(dim, T):
+    """ops.linear(o, W, None, xshift=v): forward o W^T, weight gradient g^T (o + v) -- the proj
+    Linear of a block whose v_bias was folded into the bias (swinv2.py:255-262)."""
+    import hvamd.ops as ops
+    torch.manual_seed(dim)
+    o = torch.randn(T, dim, device="cuda").bfloat16()
+    W = torch.nn.Parameter(torch.randn(dim, dim, device="cuda") / dim ** 0.5)
+    v = torch.randn(dim, device="cuda")
+    g = torch.randn(T, dim, device="cuda").bfloat16()
+    y = ops.linear(o, W, None, xshift=v)
+    y.backward(g)
+    ref = g.float().t() @ (o.float() + v[None, :])
+    assert ((W.grad - ref).norm() / ref.norm()).item() < 1e-4
+    W.grad = None
+    ops.linear(o, W, None).backward(g)
+    ref0 = g.float().t() @ o.float()
+    assert ((W.grad - ref0).norm() / ref0.norm()).item() < 1e-4
 
 
 @pytest.mark.parametrize("B,T,C", [(256, 49, 768), (3, 5, 256), (2, 64, 1024), (4, 7, 1536)])

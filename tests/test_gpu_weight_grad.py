@@ -10,7 +10,8 @@ pytestmark = pytest.mark.gpu
 CASES = [(288, 96, 32 * 517), (96, 96, 6272), (384, 96, 12544), (96, 384, 12544),
          (576, 192, 3136), (192, 192, 800), (768, 192, 3136), (192, 768, 3136),
          (1152, 384, 1568), (384, 384, 1568), (1536, 384, 1568), (384, 1536, 1568),
-         (2304, 768, 12544), (768, 3072, 2048), (192, 384, 6272), (384, 768, 1568), (32 * 6, 192, 32)]
+         (2304, 768, 12544), (768, 3072, 2048), (192, 384, 6272), (384, 768, 1568), (32 * 6, 192, 32),
+         (96, 48, 32 * 999)]
 
 
 def _ref(g, x):
@@ -97,3 +98,28 @@ def test_linear_backward_uses_weight_grad_kernel():
     rw = g2.float().t() @ x.detach().reshape(-1, 192).float()
     assert ((w.grad - rw).norm() / rw.norm()).item() < 1e-5
     assert ((b.grad - g2.float().sum(0)).norm() / b.grad.norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("N,K,M", [(96, 96, 6272), (384, 384, 1568), (768, 768, 2048), (192, 192, 800)])
+@pytest.mark.parametrize("with_db", [True, False])
+def test_weight_grad_shift_matches_fp32(N, K, M, with_db):
+    """hvk_weight_grad_shift: dW = g^T (x + 1 xshift^T) (the proj Linear with v_bias folded into its
+    bias), db = sum g, against fp32 of the same bf16 operands; bit-identical db to the plain
+    kernel's."""
+    from hvamd import _lib
+    lib = _lib.load()
+    gen = torch.Generator(device="cuda").manual_seed(N + K + M)
+    g = torch.randn(M, N, device="cuda", generator=gen).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=gen).bfloat16()
+    xs = torch.randn(K, device="cuda", generator=gen)
+    dw = torch.full((N, K), float("nan"), device="cuda")
+    db = torch.full((N,), float("nan"), device="cuda") if with_db else None
+    ws = torch.empty(lib.hvk_weight_grad_workspace(M, N, K), device="cuda", dtype=torch.uint8)
+    _lib.call("hvk_weight_grad_shift", _lib.ptr(g), _lib.ptr(x), _lib.ptr(xs), _lib.ptr(dw),
+              _lib.ptr(db) if with_db else None, M, N, K, _lib.ptr(ws), ws.numel(), _lib.stream())
+    torch.cuda.synchronize()
+    rw = g.float().t() @ (x.float() + xs[None, :])
+    err = (dw - rw).abs().max().item()
+    assert err <= 1e-4 * M ** 0.5 * 4 * (1 + xs.abs().max().item()), err
+    if with_db:
+        assert (db - g.float().sum(0)).abs().max().item() <= 1e-4 * M ** 0.5 * 4

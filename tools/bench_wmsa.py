@@ -86,7 +86,7 @@ def main():
         normed = args.normed and win <= 8
         rn = torch.empty(T, 2 * nh, device="cuda")
         if normed:
-            _lib.call("hvk_qk_normalize", P(qkv), P(rn), T, C, st())
+            _lib.call("hvk_qk_normalize", P(qkv), P(rn), P(scale), T, C, st())
 
         def fwd():
             if normed:

@@ -6,7 +6,9 @@ after the MFMA was found padded with 2 states instead of 8 (wmsa_ring.hip: the u
 path skipping the mask block read the scores too early; wrong values, no fault).  This walks
 every path from each MFMA (fallthrough and taken branches) and reports any instruction that
 touches the MFMA's destination registers within MIN_STATES wait states (an MFMA taking the
-whole destination as its accumulator C is the legal chain and is skipped).
+whole destination as its accumulator C is the legal chain and is skipped, and so is the same
+MFMA opcode overwriting without reading part of the destination: XDL results retire in issue
+order; the remaining registers stay watched).
 
     python tools/mfma_hazard_audit.py [--states 8] file.hip ...   (default: every csrc/*.hip)
 """
@@ -70,30 +72,37 @@ def audit(lines, labels, min_states):
         if not mn.startswith("v_mfma"):
             continue
         fields = [f.strip() for f in ops.split(",")]
-        dst = regs(fields[0])
         seen = set()
-        work = [(i + 1, 0)]
+        work = [(i + 1, 0, frozenset(regs(fields[0])))]
         while work:
-            j, st = work.pop()
-            while j < len(lines) and st < min_states:
-                if (j, st) in seen:
+            j, st, dst = work.pop()
+            while j < len(lines) and st < min_states and dst:
+                if (j, st, dst) in seen:
                     break
-                seen.add((j, st))
+                seen.add((j, st, dst))
                 m2, o2 = lines[j]
                 f2 = [f.strip() for f in o2.split(",")]
                 touched = regs(o2) & dst
                 if touched:
-                    ok = m2.startswith("v_mfma") and len(f2) >= 4 and regs(f2[3]) == dst and not (
-                        (regs(f2[1]) | regs(f2[2])) & dst)
-                    if not ok:
+                    is_mfma = m2.startswith("v_mfma") and len(f2) >= 4
+                    reads = (regs(f2[1]) | regs(f2[2]) | regs(f2[3])) & dst if is_mfma else touched
+                    if is_mfma and regs(f2[3]) == dst and not ((regs(f2[1]) | regs(f2[2])) & dst):
+                        break  # the accumulation chain: C = the whole earlier destination
+                    if is_mfma and not reads and m2 == mn:
+                        # the same XDL opcode overwriting (not reading) part of the destination:
+                        # XDL results retire in issue order, so the later write wins (LLVM's
+                        # hazard recognizer pads no XDL -> XDL write-after-write of equal passes);
+                        # the earlier MFMA's remaining registers stay under watch
+                        dst = dst - frozenset(regs(f2[0]))
+                    else:
                         bad.append((i, j, st, mn, m2 + " " + o2))
-                    break
+                        break
                 if m2 == "s_endpgm":
                     break
                 if m2.startswith("s_cbranch") or m2 == "s_branch":
                     tgt = labels.get(o2.strip())
                     if tgt is not None:
-                        work.append((tgt, st + 1))
+                        work.append((tgt, st + 1, dst))
                     if m2 == "s_branch":
                         break
                 st += states(m2, o2)
