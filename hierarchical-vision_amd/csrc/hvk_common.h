@@ -18,7 +18,7 @@ typedef unsigned short hvk_bf16;  // raw bf16 bits in memory
 #ifdef __cplusplus
 extern "C" {
 #endif
-int hvk_set_error(int code, const char* fmt, ...);
+__attribute__((visibility("hidden"))) int hvk_set_error(int code, const char* fmt, ...);
 #ifdef __cplusplus
 }
 #endif
@@ -60,7 +60,8 @@ int hvk_set_option(const char* name, long long value, long long* previous);
 extern "C" {
 #endif
 // null pair: not timed; work = the launch's algorithmic flops (or bytes), summed by read
-void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop);
+__attribute__((visibility("hidden"))) void hvk_timer_next(int kind, double work, hipEvent_t* start,
+                                                     hipEvent_t* stop);
 #ifdef __cplusplus
 }
 #endif

@@ -3,6 +3,7 @@ goldens), config layering, algorithms, model surface and state-dict parity."""
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -24,6 +25,11 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert set(declared) == set(_lib.SIGNATURES), set(declared) ^ set(_lib.SIGNATURES)
+    # and nothing else: internal helpers are hidden, so the export table IS the ABI
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True)
+    if nm.returncode == 0:
+        exported = {ln.split()[-1] for ln in nm.stdout.splitlines() if " T hvk_" in ln}
+        assert exported == set(declared), exported ^ set(declared)
     lib = _lib.load()
     assert lib.hvk_abi_version() == 9
     # [accumulators][dscale nH][dq_bias 32 nH] floats
