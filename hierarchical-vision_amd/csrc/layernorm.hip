@@ -20,6 +20,10 @@
 // rows at once, grid-strided.  Row statistics are TPR-lane xor-shuffle reductions.
 #include "hvk_common.h"
 
+#ifndef HVK_LN_X0_EARLY  // A/B build switch: residual loads issued with the branch-output loads
+#define HVK_LN_X0_EARLY 1  // (up to TPR = 16, i.e. C <= 128: tools/bench_ln.py, profiles/round4/ln_ab)
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;
@@ -90,8 +94,20 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
   for (int row = (blockIdx.x * kWaves + wave) * RPW + sub; row < p.rows;
        row += gridDim.x * kWaves * RPW) {
     const size_t rb = (size_t)row * p.C;
-    float v[EPT];
+    float v[EPT], x0v[EPT];
     float s = 0.f;
+    // the residual row loaded with the branch output, before the statistics: one memory round
+    // trip per row instead of two (+EPT VGPRs).  Stage 0 (C = 96, 4 rows per wave) -1.4 %, the
+    // 1-2-row-per-wave layouts of C >= 192 +6-12 % (tools/bench_ln.py): there it stays after
+    constexpr bool early = HVK_LN_X0_EARLY && TPR <= 16;
+    if constexpr (early) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x0v[4 * i + j] = 0.f;
+        if (ok[i] && p.x0) ld4_f32_stream(p.x0 + rb + grp_c<TPR>(t, i), x0v + 4 * i);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       if (ok[i]) {
@@ -118,7 +134,12 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
       if (!ok[i]) continue;
       const int c = grp_c<TPR>(t, i);
       float r[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.x0) ld4_f32_stream(p.x0 + rb + c, r);
+      if constexpr (early) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = x0v[4 * i + j];
+      } else if (p.x0) {
+        ld4_f32_stream(p.x0 + rb + c, r);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] += ((v[4 * i + j] - mu) * rs * gm[4 * i + j] + bt[4 * i + j]) * sc;
       st4_f32(p.x + rb + c, r, HVK_NT_SAVED & 2);  // the f32 stream is read again only at the next LayerNorm

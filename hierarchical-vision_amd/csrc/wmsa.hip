@@ -110,12 +110,15 @@ __device__ __forceinline__ uint32_t mask_bits(uint32_t krow, uint32_t kcol, int 
 }
 
 // Backward P / dS images [query][key] (ROWS bf16 per row = ROWS/4 8-B units): the 8-B unit
-// col8 of `row` is stored at col8 ^ f(row), f = (r0^r2) | r3<<1 | r1<<2: the 8-B writes of a
-// query tile and the transposed reads of phase B are then bank-conflict free.
-template <int ROWS>
-__device__ __forceinline__ int pimg_off(int row, int col8) {
-  const int f = ((row ^ (row >> 2)) & 1) | ((row >> 2) & 2) | ((row << 1) & 4);
-  return row * ROWS + (((col8 ^ f) & (ROWS / 4 - 1)) << 2);
+// col8 of `row` is stored at col8 ^ pswz(row), pswz a bijection of the row's low 4 bits with
+// bits 3:2 = (row >> 1) & 3 and bits 1:0 = (row >> 3 & 1, row & 1).  Under the LDS bank model
+// (MI355X_MICROARCH.md §LDS): phase A's ds_write_b64 (16 lanes = the 16 rows of a query tile, one
+// unit each, banks mod 32 = one 128-B row) needs 16 distinct units per tile -> a bijection; phase
+// B's transposed reads (32 lanes = rows 4gq + li/4 of one 8-row block x units 4kt + li%4, banks
+// mod 64 = two rows) need bits 3:2 distinct over the 4 rows of one parity.  The 3-bit form of
+// round 3 left both 2-way (≈25 % of the kernel's LDS cycles, matching SQ_LDS_BANK_CONFLICT).
+__device__ __forceinline__ int pswz(int row) {
+  return (((row >> 1) & 3) << 2) | (((row >> 3) & 1) << 1) | (row & 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -247,12 +250,13 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   const int o_row = fm16(li, gq);                       // 16-B unit gq of token row li
   const int o_r8 = fm8(li, gq);                         // 8-B unit gq of token row li
   const int o_kt = fm8(4 * gq + (li >> 2), li & 3);     // tr-read of rows 4gq + li/4, unit li&3
-  // P / dS images: row q = 16qi + li, 8-B unit 4ki + gq stored at unit (4ki + gq) ^ f(li)
-  const int fli = ((li ^ (li >> 2)) & 1) | ((li >> 2) & 2) | ((li << 1) & 4);
-  const int o_pw0 = li * ROWS * 2 + ((gq ^ fli) << 3), o_pw1 = li * ROWS * 2 + ((4 ^ gq ^ fli) << 3);
+  // P / dS images: row q = 16qi + li, 8-B unit 4ki + gq stored at unit (4ki + gq) ^ pswz(li)
+  // = 4ki ^ (gq ^ pswz(li)): byte offset (row base | unit) ^ 32 ki, the row base a multiple of
+  // the row's bytes (one register; one v_xor per write)
+  const int o_pw = li * ROWS * 2 + (((gq ^ pswz(li)) & (ROWS / 4 - 1)) << 3);
   // phase B transposed reads: row rq = 4gq + li/4 (+16m + 32c), unit 4kt + (li&3)
   const int rq0 = 4 * gq + (li >> 2);
-  const int frq = ((rq0 ^ (rq0 >> 2)) & 1) | ((rq0 >> 2) & 2) | ((rq0 << 1) & 4);
+  const int frq = pswz(rq0);
   const int o_trq = fm8(rq0, li & 3);
 
   hvk_f32x4 dbias[TPW][NT];
@@ -441,8 +445,9 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
           }
           dsp[ki][0] = hvk_pack2(ds[0], ds[1]);
           dsp[ki][1] = hvk_pack2(ds[2], ds[3]);
-          // unit (4ki + gq) ^ f = 4(ki ^ f>>2) + (gq ^ f&3): base 0 / 1 by ki&1, +64 B for ki >= 2
-          const int off = qi * 16 * ROWS * 2 + ((ki & 1) ? o_pw1 : o_pw0) + 64 * (ki >> 1);
+          int pw = o_pw;  // the xor per write, not four hoisted offsets held across the loop
+          asm volatile("" : "+v"(pw));
+          const int off = qi * 16 * ROWS * 2 + (pw ^ (32 * ki));
           *reinterpret_cast<uint2*>((char*)ps + off) =
               make_uint2(hvk_pack2(p[ki][0] * inv, p[ki][1] * inv), hvk_pack2(p[ki][2] * inv, p[ki][3] * inv));
           *reinterpret_cast<uint2*>((char*)dss + off) = make_uint2(dsp[ki][0], dsp[ki][1]);
