@@ -28,6 +28,9 @@
 #ifndef HVK_TILE_PRIO  // A/B build: s_setprio 1 over each k-step's MFMAs
 #define HVK_TILE_PRIO 0
 #endif
+#ifndef HVK_TILE_STAGED  // 1: the 128-row tiles store their outputs through LDS as whole row runs
+#define HVK_TILE_STAGED 1
+#endif
 #if HVK_GEMM_PROBE == 4
 __device__ unsigned long long g_gemm_probe[32768 * 6];
 #endif
@@ -54,6 +57,12 @@ __device__ __forceinline__ int perm_row(int p) {
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
+// workgroup barrier that waits only for this wave's LDS operations (stores in flight stay)
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -93,15 +102,60 @@ __device__ __forceinline__ void load_h_tile(uint4 (&hp)[EPI == 2 ? HM : 1][NT / 
   }
 }
 
+// LDS-staged output (128-row tiles): a fragment store from registers writes 16 rows x 64 B per
+// wave-instruction (16 half lines); staged through the tile's LDS, which the k-loop no longer
+// uses, each 256-thread store round writes 4 KB of whole row runs (cdna_hip_programming.md:
+// "O staged through LDS and stored as whole rows").  Image [BM rows][BN bf16], the 16-B chunk
+// cc of row r at cc ^ (r & 7): the fragment writes (8-lane groups = 8 rows, one chunk) and the
+// row-run reads are bank-conflict free under the §LDS model of MI355X_MICROARCH.md.
+template <int BN>
+__device__ __forceinline__ uint32_t stage_off(int row, int cc) {
+  return (uint32_t)(row * BN * 2 + 16 * (cc ^ (row & 7)));
+}
+template <int NT, int MT, int BN>
+__device__ __forceinline__ void stage_write(char* smem, const hvk_u32x4 (&v)[MT][NT / 2], int r0, int c0) {
+  const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
+#pragma unroll
+  for (int b = 0; b < MT; ++b)
+#pragma unroll
+    for (int j = 0; j < NT / 2; ++j)
+      *reinterpret_cast<hvk_u32x4*>(smem + stage_off<BN>(r0 + 16 * b + li, c0 + 4 * j + gq)) = v[b][j];
+}
+// every 16-B chunk of the 128 x BN image -> Y rows m0 .., columns n0 ..: all LDS reads first,
+// then the stores back to back
+template <int BN, bool NTS>
+__device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restrict__ Y, int M, int N, int m0, int n0) {
+  constexpr int CPR = BN / 8, PER = 128 * CPR / 256;
+  static_assert(128 * CPR % 256 == 0, "whole store rounds");
+  hvk_u32x4 v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i, row = c / CPR, cc = c - row * CPR;
+    v[i] = *reinterpret_cast<const hvk_u32x4*>(smem + stage_off<BN>(row, cc));
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + 256 * i, row = c / CPR, cc = c - row * CPR;
+    if (m0 + row < M) {
+      hvk_u32x4* dst = reinterpret_cast<hvk_u32x4*>(Y + (size_t)(m0 + row) * N + n0 + 8 * cc);
+      if (NTS) __builtin_nontemporal_store(v[i], dst);
+      else *dst = v[i];
+    }
+  }
+}
+
 // EPI 4 (the qkv Linear of a w <= 8 W-MSA block): Y = acc + bias with every q and k head slice
 // (columns < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
 // 1 / max(||x||, eps) stored to rn [M, 2N/96]; the v columns as EPI 0.
-template <int EPI, int NT, int MT, int HPRE = 0>
+template <int EPI, int NT, int MT, int HPRE = 0, int SBN = 0>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
                                               int N, int row0, int col0,
                                               const uint4 (*hpre)[NT / 2] = nullptr, float* __restrict__ rn = nullptr,
-                                              const float* __restrict__ qscale = nullptr) {
+                                              const float* __restrict__ qscale = nullptr, char* smem = nullptr,
+                                              int m0 = 0, int n0 = 0) {
+  // SBN > 0: outputs staged through the LDS image of a 128 x SBN tile whose origin is (m0, n0)
+  // (every wave of the workgroup calls this; the k-loop's LDS reads are all complete)
   // HPRE: h of token tiles 0 .. HPRE-1 was loaded early by the caller (hpre)
   const int lane = threadIdx.x & 63, li = lane & 15, gq = lane >> 4;
   float bv[NT / 2][8];
@@ -180,12 +234,25 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
       asm volatile("" : "+v"(pk[b][j]));
       if (EPI == 1) asm volatile("" : "+v"(pg[b][j]));
     }
+  if constexpr (SBN > 0) {
+    const int r0 = row0 - m0, c0 = (col0 - n0) / 8;
+    stage_write<NT, MT, SBN>(smem, pk, r0, c0);
+    lds_sync();
+    stage_store<SBN, EPI == 1 && (HVK_NT_SAVED & 1)>(smem, Y, M, N, m0, n0);  // h: read again only by the backward
+    if constexpr (EPI == 1) {
+      lds_sync();  // every thread's image reads are back before the GELU outputs overwrite it
+      stage_write<NT, MT, SBN>(smem, pg, r0, c0);
+      lds_sync();
+      stage_store<SBN, false>(smem, Y2, M, N, m0, n0);
+    }
+  }
 #pragma unroll
   for (int b = 0; b < MT; ++b) {
     const int row = row0 + 16 * b + li;
     if (row >= M) continue;
 #pragma unroll
     for (int j = 0; j < NT / 2; ++j) {
+      if constexpr (SBN > 0) break;
       const size_t o = (size_t)row * N + col0 + 32 * j + 8 * gq;
       if (EPI == 1 && (HVK_NT_SAVED & 1))  // h: read again only by the backward
         __builtin_nontemporal_store(pk[b][j], reinterpret_cast<hvk_u32x4*>(Y + o));
@@ -354,7 +421,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  tile_epilogue<EPI, TN, 4, HPB>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn, qscale);
+  tile_epilogue<EPI, TN, 4, HPB, HVK_TILE_STAGED ? BN : 0>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre,
+                                                         rn, qscale, smem, m0, n0);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
