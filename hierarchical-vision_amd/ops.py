@@ -242,13 +242,18 @@ def _native_nt(M, K, N):
     return _tile_ok(M, K, N) or _linear_native(M, K, N)
 
 
+# fc1 + GELU widths on the skinny kernel (stage 0 outside the fused MLP; stage 1 unless
+# HVK_S1_GELU_TILE=1 routes it to the tiled EPI 1 kernel, A/B runs)
+_GELU_SKINNY_K = (96,) if os.environ.get("HVK_S1_GELU_TILE", "0") == "1" else (96, 192)
+
+
 def gelu_fwd(x2, wb, bias):
     """(h, GELU(h)) with h = x2 wb^T + bias as ONE kernel (fc1 of swinv2.py:58-62), or None
     when no fused kernel is built for the shape."""
     M, K = x2.shape
     N = wb.shape[0]
     lib = _lib.load()
-    if (K in (96, 192) or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N):
+    if (K in _GELU_SKINNY_K or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N):
         fn = "hvk_linear_gelu_fwd"
     elif _tile_ok(M, K, N):
         fn = "hvk_gemm_gelu_fwd"
