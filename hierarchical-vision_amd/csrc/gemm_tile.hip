@@ -674,12 +674,14 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
 template <int EPI>
 int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                 int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr) {
-  // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1536 case
+  // 128 x 192 also where 192 | N and the tile is not the narrow N = 384, K < 1152 case
   // (tools/bench_gemm.py, interleaved: 3-25 % faster on the stage-2/3 shapes, 6 % slower on
-  // the stage-2 projection); option "tile_wide" 0 / 1 forces 128 / 192 columns where both divide N
+  // the stage-2 projection; with the LDS-staged epilogue also 5 % faster for the stage-2 qkv
+  // input gradient, K = 1152: profiles/round4/tile_width_staged/); option "tile_wide" 0 / 1
+  // forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
   if constexpr (EPI == 4) {  // the qkv form: the 128-row tile kernel only
-    if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1536)))
+    if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1152)))
       return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
   } else {
@@ -696,7 +698,7 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   // (tools/gpu_tilew.sh: 2-7 % on s2/s3 fc1; 192 stays faster for stage-1 fc1 and for EPI 2)
   const bool epi1_narrow = EPI == 1 && K >= 384 && N % TileCfg<4>::BN == 0;
   const bool wide = N % TileCfg<6>::BN == 0 &&
-                    (force >= 0 ? force == 1 : ((N > 384 || K >= 1536) && !epi1_narrow));
+                    (force >= 0 ? force == 1 : ((N > 384 || K >= 1152) && !epi1_narrow));
   if (N % TileCfg<4>::BN == 0 && !wide)
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st);
   return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st);

@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--only", default=None, help="regex of gemm names to run")
     ap.add_argument("--lib", default=None, help="load this libhvk build instead (tools/probe)")
     ap.add_argument("--model", default="t", choices=sorted(MODELS), help="stage shapes: t, b224, b384")
+    ap.add_argument("--option", action="append", default=[], help="libhvk option NAME=VALUE (hvk_set_option)")
     a = ap.parse_args()
     if a.lib:
         from hvamd import _lib as L
@@ -70,6 +71,10 @@ def main():
     floor = {"fwd": 0.0, "dx": 0.0, "dw": 0.0}
     from hvamd import _lib
     lib = _lib.load()
+    import ctypes
+    for o in a.option:
+        k, v = o.split("=")
+        assert lib.hvk_set_option(k.encode(), int(v), ctypes.byref(ctypes.c_longlong())) == 0, o
     tot_h = 0.0
     print(f"{'gemm':10s} {'M':>7s} {'K':>5s} {'N':>6s} {'n':>2s} | {'fwd us':>8s} {'dx us':>8s} {'dw us':>8s} | floor(us) fwd/dx/dw | hvk fwd/dx us | tile fwd/dx us")
     import re
