@@ -40,6 +40,24 @@ __device__ __forceinline__ int perm_row(int p) {
   return 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3);
 }
 
+#ifndef HVK_LIN_PAIRSTORE  // 1: output slices stored in row pairs as whole 128-B lines (A/B switch)
+#define HVK_LIN_PAIRSTORE 1
+#endif
+// Full-line output stores: lane (li, g) holds columns 32j + 8g .. +7 of row li for every slice j,
+// so a plain store writes 16 rows x 64 B (16 half lines).  For a slice pair (j, j+1), rows li and
+// li ^ 8 swap halves (one DPP row_ror:8 per dword): lanes li < 8 then hold (row li, j) and
+// (row li + 8, j), lanes li >= 8 (row li - 8, j+1) and (row li, j+1) -- two stores of 8 rows x
+// 128 B each, every line written whole by one instruction.
+__device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void pair_rows(const uint4& v0, const uint4& v1, bool lo, uint4& a, uint4& b) {
+  const uint4 x = lo ? v1 : v0;
+  const uint4 r = make_uint4(dpp_ror8(x.x), dpp_ror8(x.y), dpp_ror8(x.z), dpp_ror8(x.w));
+  a = lo ? v0 : r;
+  b = lo ? r : v1;
+}
+
 // EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
 // bf16 pre-activation kept for the backward and the activation for fc2 (the reference's
 // F.linear(+bias) -> nn.GELU on the bf16 tensor, swinv2.py:58-62).
@@ -155,6 +173,39 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
       const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N * 2);
       const auto ry2 = hvk_tile_rsrc(Y2, 16 * tile, M, N * 2);
       const uint32_t yo = (uint32_t)(li * N + n0 + 8 * g) * 2;
+      // pair stores: rows li & 7 (+8), the j+1 half for lanes li >= 8
+      const bool lo8 = li < 8;
+      const uint32_t yp = (uint32_t)((li & 7) * N + n0 + 8 * g + (lo8 ? 0 : 32)) * 2;
+      uint4 pend = make_uint4(0, 0, 0, 0), pend2 = make_uint4(0, 0, 0, 0);  // slice j-1 (j odd)
+      // store slice j (value v, second output v2 for EPI 1) now or as the second of a pair
+      auto put = [&](int j, const uint4& v, const uint4& v2, bool nt) {
+        if (!HVK_LIN_PAIRSTORE || (j % 2 == 0 && j + 1 >= G::NT / 2)) {  // unpaired last slice
+          if (nt) hvk_bst16_nt(ry, yo + 64 * j, v);
+          else hvk_bst16(ry, yo + 64 * j, v);
+          if (EPI == 1) hvk_bst16(ry2, yo + 64 * j, v2);
+          return;
+        }
+        if (j % 2 == 0) {
+          pend = v;
+          pend2 = v2;
+          return;
+        }
+        uint4 a0, b0;
+        pair_rows(pend, v, lo8, a0, b0);
+        const uint32_t o = yp + 64 * (j - 1);
+        if (nt) {
+          hvk_bst16_nt(ry, o, a0);
+          hvk_bst16_nt(ry, o + 16 * N, b0);
+        } else {
+          hvk_bst16(ry, o, a0);
+          hvk_bst16(ry, o + 16 * N, b0);
+        }
+        if (EPI == 1) {
+          pair_rows(pend2, v2, lo8, a0, b0);
+          hvk_bst16(ry2, o, a0);
+          hvk_bst16(ry2, o + 16 * N, b0);
+        }
+      };
       float rq[EPI == 4 ? G::NT / 2 : 1];  // EPI 4: the row's 1/||x|| per head slice
 #pragma unroll
       for (int j = 0; j < (EPI == 4 ? G::NT / 2 : 1); ++j) rq[j] = 0.f;
@@ -176,7 +227,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             v[e + 1] *= d.y;
           }
           const uint4 gv = hvk_pack8(v);
-          hvk_bst16(ry, yo + 64 * j, gv);
+          put(j, gv, gv, false);
           float r[8];
           hvk_unpack8(gv, r);  // the bias gradient sums the stored (rounded) gradient (0 past M)
 #pragma unroll
@@ -200,10 +251,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             rq[j] = r;
           }
         }
-        if (EPI == 1 && (HVK_NT_SAVED & 1))
-          hvk_bst16_nt(ry, yo + 64 * j, hv);
-        else
-          hvk_bst16(ry, yo + 64 * j, hv);
+        uint4 gl = hv;
         if (EPI == 1) {
           float u[8];
           hvk_unpack8(hv, u);  // GELU of the rounded pre-activation, as the reference
@@ -213,8 +261,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
             u[e] = y.x;
             u[e + 1] = y.y;
           }
-          hvk_bst16(ry2, yo + 64 * j, hvk_pack8(u));
+          gl = hvk_pack8(u);
         }
+        put(j, hv, gl, EPI == 1 && (HVK_NT_SAVED & 1));
       }
       if constexpr (EPI == 4) {
         // the row's 1/||x|| per q / k head slice j (all 4 lanes of a row hold every one): lane g
@@ -324,6 +373,10 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
     const auto rh = hvk_tile_rsrc(H, 16 * tile, M, N1 * 2), rg2 = hvk_tile_rsrc(Gh, 16 * tile, M, N1 * 2);
     const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N2 * 2);
     const uint32_t ho = (uint32_t)(li * N1 + 8 * g) * 2, yo = (uint32_t)(li * N2 + 8 * g) * 2;
+    const bool lo8 = li < 8;
+    const uint32_t hp = (uint32_t)((li & 7) * N1 + 8 * g + (lo8 ? 0 : 32)) * 2;
+    const uint32_t yp = (uint32_t)((li & 7) * N2 + 8 * g + (lo8 ? 0 : 32)) * 2;
+    uint4 ph = make_uint4(0, 0, 0, 0), pg = ph;
     hvk_f32x4 acc[G1::NT];
 #pragma unroll
     for (int t = 0; t < G1::NT; ++t) acc[t] = hvk_f32x4{0, 0, 0, 0};
@@ -344,11 +397,30 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
       }
       const uint4 hv = hvk_pack8(v);
       const uint4 gv = hvk_gelu8_bf16(hv);  // GELU of the rounded pre-activation, as the reference
-      if (HVK_NT_SAVED & 1)
-        hvk_bst16_nt(rh, ho + 64 * j, hv);
-      else
-        hvk_bst16(rh, ho + 64 * j, hv);
-      hvk_bst16(rg2, ho + 64 * j, gv);
+      if (!HVK_LIN_PAIRSTORE) {
+        if (HVK_NT_SAVED & 1)
+          hvk_bst16_nt(rh, ho + 64 * j, hv);
+        else
+          hvk_bst16(rh, ho + 64 * j, hv);
+        hvk_bst16(rg2, ho + 64 * j, gv);
+      } else if (j % 2 == 0) {  // whole-line row-pair stores (see pair_rows)
+        ph = hv;
+        pg = gv;
+      } else {
+        uint4 a0, b0;
+        const uint32_t o = hp + 64 * (j - 1);
+        pair_rows(ph, hv, lo8, a0, b0);
+        if (HVK_NT_SAVED & 1) {
+          hvk_bst16_nt(rh, o, a0);
+          hvk_bst16_nt(rh, o + 16 * N1, b0);
+        } else {
+          hvk_bst16(rh, o, a0);
+          hvk_bst16(rh, o + 16 * N1, b0);
+        }
+        pair_rows(pg, gv, lo8, a0, b0);
+        hvk_bst16(rg2, o, a0);
+        hvk_bst16(rg2, o + 16 * N1, b0);
+      }
       // fc2 k-chunk j: this lane's GELU(h) of hidden units 32j + 8g .. +7 is the B fragment
 #pragma unroll
       for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
@@ -363,7 +435,17 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += b2l[32 * j + 8 * g + e];  // 0 without a bias
-      hvk_bst16(ry, yo + 64 * j, hvk_pack8(v));
+      const uint4 yv = hvk_pack8(v);
+      if (!HVK_LIN_PAIRSTORE || j == G2::NT / 2 - 1) {  // the third slice stores alone
+        hvk_bst16(ry, yo + 64 * j, yv);
+      } else if (j % 2 == 0) {
+        ph = yv;
+      } else {
+        uint4 a0, b0;
+        pair_rows(ph, yv, lo8, a0, b0);
+        hvk_bst16(ry, yp + 64 * (j - 1), a0);
+        hvk_bst16(ry, yp + 64 * (j - 1) + 16 * N2, b0);
+      }
     }
 #pragma unroll
     for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
@@ -436,6 +518,10 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __r
     __builtin_amdgcn_sched_barrier(0);
     const auto rgh = hvk_tile_rsrc(GH, 16 * tile, M, N1 * 2), rgx = hvk_tile_rsrc(GX, 16 * tile, M, N2 * 2);
     const uint32_t ho = (uint32_t)(li * N1 + 8 * g) * 2, xo = (uint32_t)(li * N2 + 8 * g) * 2;
+    const bool lo8 = li < 8;
+    const uint32_t hp = (uint32_t)((li & 7) * N1 + 8 * g + (lo8 ? 0 : 32)) * 2;
+    const uint32_t xp = (uint32_t)((li & 7) * N2 + 8 * g + (lo8 ? 0 : 32)) * 2;
+    uint4 ph = make_uint4(0, 0, 0, 0);
     hvk_f32x4 acc2[G2::NT];
 #pragma unroll
     for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_f32x4{0, 0, 0, 0};
@@ -467,7 +553,16 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __r
           v[e + 1] *= d.y;
         }
         const uint4 gv = hvk_pack8(v);
-        hvk_bst16(rgh, ho + 64 * j, gv);
+        if (!HVK_LIN_PAIRSTORE) {
+          hvk_bst16(rgh, ho + 64 * j, gv);
+        } else if (jj % 2 == 0) {  // whole-line row-pair stores (see pair_rows)
+          ph = gv;
+        } else {
+          uint4 a0, b0;
+          pair_rows(ph, gv, lo8, a0, b0);
+          hvk_bst16(rgh, hp + 64 * (j - 1), a0);
+          hvk_bst16(rgh, hp + 64 * (j - 1) + 16 * N1, b0);
+        }
 #pragma unroll
         for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
       }
@@ -480,7 +575,17 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_bwd_kernel(const hvk_bf16* __r
         v[r] = acc2[2 * j][r];
         v[4 + r] = acc2[2 * j + 1][r];
       }
-      hvk_bst16(rgx, xo + 64 * j, hvk_pack8(v));
+      const uint4 xv = hvk_pack8(v);
+      if (!HVK_LIN_PAIRSTORE || j == G2::NT / 2 - 1) {
+        hvk_bst16(rgx, xo + 64 * j, xv);
+      } else if (j % 2 == 0) {
+        ph = xv;
+      } else {
+        uint4 a0, b0;
+        pair_rows(ph, xv, lo8, a0, b0);
+        hvk_bst16(rgx, xp + 64 * (j - 1), a0);
+        hvk_bst16(rgx, xp + 64 * (j - 1) + 16 * N2, b0);
+      }
     }
 #pragma unroll
     for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
