@@ -48,15 +48,6 @@ __device__ __forceinline__ int perm_row(int p) {
 // li ^ 8 swap halves (one DPP row_ror:8 per dword): lanes li < 8 then hold (row li, j) and
 // (row li + 8, j), lanes li >= 8 (row li - 8, j+1) and (row li, j+1) -- two stores of 8 rows x
 // 128 B each, every line written whole by one instruction.
-__device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
-}
-__device__ __forceinline__ void pair_rows(const uint4& v0, const uint4& v1, bool lo, uint4& a, uint4& b) {
-  const uint4 x = lo ? v1 : v0;
-  const uint4 r = make_uint4(dpp_ror8(x.x), dpp_ror8(x.y), dpp_ror8(x.z), dpp_ror8(x.w));
-  a = lo ? v0 : r;
-  b = lo ? r : v1;
-}
 
 // EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
 // bf16 pre-activation kept for the backward and the activation for fc2 (the reference's

@@ -193,6 +193,24 @@ __device__ __forceinline__ uint4 hvk_bld16_nt(__amdgpu_buffer_rsrc_t r, uint32_t
 }
 // pin a value as "defined here" (after an explicit s_waitcnt): the compiler then tracks no
 // pending memory operation on its registers
+// Whole-line row pairs for register-resident 16-row tiles (lane (li, g) holding 16 B of row li per
+// 32-column slice): rows li and li ^ 8 swap one slice of a pair with a DPP row_ror:8 per dword.
+// pair_rows before a store: (v0, v1) = slices (s, s+1) of row li -> a = (row li & 7, s | s+1 by
+// li < 8 | li >= 8), b = the same 8 rows lower (+8): each of a, b then covers 8 rows x 128 B.
+// (The mirror image for loads -- 8 x 128-B loads swapped back -- measured neutral to -2 %:
+// profiles/round4/pair_stores/pair_loads_*.)
+__device__ __forceinline__ uint32_t dpp_ror8(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint4 dpp_ror8(const uint4& v) {
+  return make_uint4(dpp_ror8(v.x), dpp_ror8(v.y), dpp_ror8(v.z), dpp_ror8(v.w));
+}
+__device__ __forceinline__ void pair_rows(const uint4& v0, const uint4& v1, bool lo, uint4& a, uint4& b) {
+  const uint4 r = dpp_ror8(lo ? v1 : v0);
+  a = lo ? v0 : r;
+  b = lo ? r : v1;
+}
+
 __device__ __forceinline__ void hvk_launder(uint4& v) {
   hvk_u32x4 t = __builtin_bit_cast(hvk_u32x4, v);
   asm volatile("" : "+v"(t));
