@@ -1,5 +1,5 @@
 """Fused MLP kernels, skinny (hvk_linear_gelu_*) vs tiled (hvk_gemm_gelu_*), on the stage shapes
-both build:  python tools/bench_mlp_tile.py"""
+both build:  python tools/bench_mlp_tile.py [tile_wide=0|1 ...]"""
 import os
 import sys
 
@@ -10,10 +10,14 @@ from tools.bench_skinny import timeit  # noqa: E402
 
 
 def main():
+    import ctypes
     from hvamd import _lib
     P, st = _lib.ptr, _lib.stream
     lib = _lib.load()
-    for M, C in [(200704, 192), (50176, 384)]:
+    for o in sys.argv[1:]:  # libhvk options NAME=VALUE (e.g. tile_wide=1)
+        k, v = o.split("=")
+        assert lib.hvk_set_option(k.encode(), int(v), ctypes.byref(ctypes.c_longlong())) == 0, o
+    for M, C in [(200704, 192), (50176, 384), (12544, 768)]:
         N = 4 * C
         x = torch.randn(M, C, device="cuda").bfloat16()
         w1 = (torch.randn(N, C, device="cuda") / C ** 0.5).bfloat16()
