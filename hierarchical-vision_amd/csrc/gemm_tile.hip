@@ -123,19 +123,19 @@ __device__ __forceinline__ void stage_write(char* smem, const hvk_u32x4 (&v)[MT]
 }
 // every 16-B chunk of the 128 x BN image -> Y rows m0 .., columns n0 ..: all LDS reads first,
 // then the stores back to back
-template <int BN, bool NTS>
+template <int BN, bool NTS, int BM_ = 128, int THREADS = 256>
 __device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restrict__ Y, int M, int N, int m0, int n0) {
-  constexpr int CPR = BN / 8, PER = 128 * CPR / 256;
-  static_assert(128 * CPR % 256 == 0, "whole store rounds");
+  constexpr int CPR = BN / 8, PER = BM_ * CPR / THREADS;
+  static_assert(BM_ * CPR % THREADS == 0, "whole store rounds");
   hvk_u32x4 v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c / CPR, cc = c - row * CPR;
+    const int c = threadIdx.x + THREADS * i, row = c / CPR, cc = c - row * CPR;
     v[i] = *reinterpret_cast<const hvk_u32x4*>(smem + stage_off<BN>(row, cc));
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + 256 * i, row = c / CPR, cc = c - row * CPR;
+    const int c = threadIdx.x + THREADS * i, row = c / CPR, cc = c - row * CPR;
     if (m0 + row < M) {
       hvk_u32x4* dst = reinterpret_cast<hvk_u32x4*>(Y + (size_t)(m0 + row) * N + n0 + 8 * cc);
       if (NTS) __builtin_nontemporal_store(v[i], dst);
@@ -147,7 +147,7 @@ __device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restri
 // EPI 4 (the qkv Linear of a w <= 8 W-MSA block): Y = acc + bias with every q and k head slice
 // (columns < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
 // 1 / max(||x||, eps) stored to rn [M, 2N/96]; the v columns as EPI 0.
-template <int EPI, int NT, int MT, int HPRE = 0, int SBN = 0>
+template <int EPI, int NT, int MT, int HPRE = 0, int SBN = 0, int SBM = 128, int STHREADS = 256>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
                                               int N, int row0, int col0,
@@ -238,12 +238,12 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
     const int r0 = row0 - m0, c0 = (col0 - n0) / 8;
     stage_write<NT, MT, SBN>(smem, pk, r0, c0);
     lds_sync();
-    stage_store<SBN, EPI == 1 && (HVK_NT_SAVED & 1)>(smem, Y, M, N, m0, n0);  // h: read again only by the backward
+    stage_store<SBN, EPI == 1 && (HVK_NT_SAVED & 1), SBM, STHREADS>(smem, Y, M, N, m0, n0);  // h: read again only by the backward
     if constexpr (EPI == 1) {
       lds_sync();  // every thread's image reads are back before the GELU outputs overwrite it
       stage_write<NT, MT, SBN>(smem, pg, r0, c0);
       lds_sync();
-      stage_store<SBN, false>(smem, Y2, M, N, m0, n0);
+      stage_store<SBN, false, SBM, STHREADS>(smem, Y2, M, N, m0, n0);
     }
   }
 #pragma unroll
@@ -613,7 +613,9 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const hvk_bf16* __restr
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // balance group 1's extra barrier
 
-  tile_epilogue<EPI, WTN, WTM>(acc, bias, Y, Y2, M, N, m0 + 16 * WTM * grp, n0 + 16 * WTN * wc);
+  tile_epilogue<EPI, WTN, WTM, 0, HVK_TILE_STAGED ? BNP : 0, BMP, 512>(acc, bias, Y, Y2, M, N, m0 + 16 * WTM * grp,
+                                                                    n0 + 16 * WTN * wc, nullptr, nullptr, nullptr,
+                                                                    smem, m0, n0);
 }
 
 template <int EPI, int WTM, int WTN>
