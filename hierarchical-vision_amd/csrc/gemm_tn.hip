@@ -215,13 +215,14 @@ __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN 
 // Linear's input is o + v_bias in the reference (swinv2.py:255-262) while the GEMM ran on o, its
 // v_bias share folded into the bias (hvk_block_bias_fwd); db[n] is re-summed from the slabs here
 // (K / 4 threads share each row's partials through L2).  db null: not stored.
-__global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict__ P, int e4,
+template <int NPH>  // chunk phases (warps of 32 threads) per workgroup
+__global__ __launch_bounds__(32 * NPH) void dw_reduce_kernel(const float4* __restrict__ P, int e4,
                                                         int ndw4, int nchunk, long pstride4,
                                                         float4* __restrict__ dw,
                                                         float4* __restrict__ db,
                                                         const float* __restrict__ xshift, int K) {
-  __shared__ float4 red[8][32];
-  __shared__ float redd[8][32];
+  __shared__ float4 red[NPH][32];
+  __shared__ float redd[NPH][32];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int e = blockIdx.x * 32 + tx;
   const int n = (4 * e) / K;  // the dW row of this float4 (e < ndw4)
@@ -230,7 +231,7 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict
   float sd = 0.f;
   if (e < e4) {
 #pragma unroll 4
-    for (int c = ty; c < nchunk; c += 8) {
+    for (int c = ty; c < nchunk; c += NPH) {
       const float4 v = P[(size_t)c * pstride4 + e];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       if (xshift && e < ndw4) sd += Pdb[(size_t)c * pstride4 * 4];
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256) void dw_reduce_kernel(const float4* __restrict
   __syncthreads();
   if (ty == 0 && e < e4) {
 #pragma unroll
-    for (int j = 1; j < 8; ++j) {
+    for (int j = 1; j < NPH; ++j) {
       const float4 v = red[j][tx];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       sd += redd[j][tx];
@@ -381,9 +382,17 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
   if (rc != HVK_OK) return rc;
   const int ndw4 = N * K / 4;
   const int e4 = wd ? (int)(p.pstride / 4) : ndw4;
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((e4 + 31) / 32)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(P), e4, ndw4, p.nchunk, p.pstride / 4,
-                     reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db), xshift, K);
+  // deep slab stacks (the stage-0 shapes: 256 chunks over few columns) get 32 chunk phases per
+  // workgroup instead of 8, so each thread's dependent chain of slab reads is 4x shorter
+  // (profiles/round4/dw_reduce_phases/: stage-0 proj / embed -1.3-2 us, 128-chunk merge +3 us)
+  if (p.nchunk >= 256)
+    hipLaunchKernelGGL(dw_reduce_kernel<32>, dim3((unsigned)((e4 + 31) / 32)), dim3(1024), 0, st,
+                       reinterpret_cast<const float4*>(P), e4, ndw4, p.nchunk, p.pstride / 4,
+                       reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db), xshift, K);
+  else
+    hipLaunchKernelGGL(dw_reduce_kernel<8>, dim3((unsigned)((e4 + 31) / 32)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(P), e4, ndw4, p.nchunk, p.pstride / 4,
+                       reinterpret_cast<float4*>(dw), reinterpret_cast<float4*>(db), xshift, K);
   HVK_CHECK_LAUNCH("hvk_weight_grad_reduce");
   return HVK_OK;
 }
