@@ -60,6 +60,8 @@ def parse():
                     help="graph mode: eager warm-up steps whose W-MSA launches are timed")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="set a libhvk option (include/hvk.h hvk_set_option) before the run; A/B runs")
+    ap.add_argument("--host-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a host routing option (hvamd.options) before the run; A/B runs")
     return ap.parse_args()
 
 
@@ -215,6 +217,41 @@ def roofline_block(kernel, nbytes, flops, ms_total, launches, steps, traffic, n_
                if n_exp else {})}
 
 
+def shape_table(launches, steps):
+    """Per-shape binding-roof table of the timed GEMM launches: grouped by (kernel, M, N, K);
+    roof = max(flops / MFMA peak, algorithmic bytes / HBM peak) per launch, binding_frac =
+    roof / measured average.  Also the whole family's binding fraction (sum of roofs / sum of
+    times), split into forward / input-gradient (kind 2) and weight-gradient (kind 3)."""
+    groups = {}
+    for r in launches:
+        key = (r["kernel"], r["M"], r["N"], r["K"], r["kind"])
+        g = groups.setdefault(key, {"ms": 0.0, "n": 0, "bytes": r["bytes"], "flops": r["flops"]})
+        g["ms"] += r["ms"]
+        g["n"] += 1
+    rows, tot = [], {2: [0.0, 0.0], 3: [0.0, 0.0]}
+    for (name, M, N, K, kind), g in groups.items():
+        avg_us = 1000.0 * g["ms"] / g["n"]
+        t_mfma = g["flops"] / (MFMA_PEAK_TFS * 1e12) * 1e6
+        t_hbm = g["bytes"] / (HBM_PEAK_GBS * 1e9) * 1e6
+        roof = max(t_mfma, t_hbm)
+        tot[kind][0] += roof * g["n"]
+        tot[kind][1] += avg_us * g["n"]
+        rows.append({"kernel": name, "M": M, "N": N, "K": K, "wgrad": kind == 3,
+                     "launches_per_step": round(g["n"] / steps, 2), "avg_us": round(avg_us, 2),
+                     "gflop": round(g["flops"] / 1e9, 2), "mbytes": round(g["bytes"] / 1e6, 1),
+                     "bound": "mfma" if t_mfma >= t_hbm else "hbm", "roof_us": round(roof, 2),
+                     "binding_frac": round(roof / avg_us, 4),
+                     "ms_per_step": round(g["ms"] / steps, 4)})
+    rows.sort(key=lambda r: -r["ms_per_step"])
+    binding = {k: {"roof_ms_per_step": round(v[0] / 1000 / steps, 3), "ms_per_step": round(v[1] / 1000 / steps, 3),
+                   "binding_frac": round(v[0] / v[1], 4) if v[1] else None}
+               for k, v in (("gemm", tot[2]), ("wgrad", tot[3]))}
+    a = tot[2][0] + tot[3][0]
+    b = tot[2][1] + tot[3][1]
+    binding["all"] = {"binding_frac": round(a / b, 4) if b else None}
+    return rows, binding
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -309,10 +346,12 @@ def main():
         if dist.get_world_size() != world:
             raise RuntimeError(f"RCCL sees {dist.get_world_size()} ranks, expected {world}")
     import hvamd.ops as ops
-    from hvamd import _lib
+    from hvamd import _lib, options
     for o in args.opt:
         name, _, val = o.partition("=")
         _lib.set_option(name, int(val))
+    for o in args.host_opt:
+        options.set(**options.parse(o))
 
     cfg, tax, model, trainer = build(args, device)
     img = model.module.patch_embed.img_size[0]
@@ -352,7 +391,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    gemm_timer, gemm_steps = None, 0
+    gemm_timer, gemm_steps, gemm_shapes = None, 0, None
     if timing and not args.graph:
         # the kernel timers run over extra steps after the timed region, so `value` is a clean
         # wall time: W-MSA launches timed by their own dispatch packets, then the GEMMs (their
@@ -369,6 +408,7 @@ def main():
         for _ in range(gemm_steps):
             step()
         torch.cuda.synchronize()
+        gemm_shapes = ops.kernel_timer_shapes()
         gemm_timer = ops.kernel_timer_stop()
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -403,6 +443,8 @@ def main():
                   "grad_bytes_per_step": 4 * sum(b[0].numel() for b in trainer.buckets.buckets)}
                  if world > 1 else None),
         "final_loss": round(loss_val, 4),
+        # every routing switch the run used: host (hvamd.options) and library (hvk_set_option)
+        "options": {"host": options.as_dict(), "lib": _lib.options()},
         # whole-step MFMA utilisation: 3 x 2 x MACs per image (forward + both backward GEMMs)
         "step_mfma": {"flops_per_step": 6 * macs * args.batch,
                       "achieved_tflops": round(6 * macs * args.batch * args.steps / elapsed / 1e12, 1),
@@ -472,6 +514,8 @@ def main():
                        "timing": ("dispatch-packet events over %d eager steps after the timed region"
                                   % gsteps if gemm_timer else
                                   "dispatch-packet events over the pre-capture eager steps")})
+        if gemm_shapes:
+            mf["shapes"], mf["binding"] = shape_table(gemm_shapes, gemm_steps)
         result["mfma"] = mf
     if rank == 0 and world == 1 and args.cpu_baseline and default_cfg:
         result["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)

@@ -7,7 +7,6 @@ is missing or a tensor is not on the GPU the call raises.
 import contextlib
 import ctypes
 import os
-import sys
 
 import torch  # noqa: F401  -- must be imported first: libhvk binds to torch's HIP runtime
 
@@ -28,6 +27,7 @@ SIGNATURES = {
     "hvk_kernel_timer_read_work": (_i, [_i, _p, _p, _p]),
     "hvk_kernel_timer_kinds": (_i, [_i]),
     "hvk_kernel_timer_launch": (_i, [_i, _p, _p, _p]),
+    "hvk_kernel_timer_launch_shape": (_i, [_i, ctypes.c_char_p, _i, _p, _p]),
     "hvk_last_error_string": (ctypes.c_char_p, []),
     "hvk_set_option": (_i, [ctypes.c_char_p, ctypes.c_longlong, _p]),
     "hvk_get_option": (_i, [ctypes.c_char_p, _p]),
@@ -105,7 +105,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 9  # include/hvk.h's HVK_ABI_VERSION this binding's SIGNATURES describe
+ABI_VERSION = 10  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
 
 
 def load():
@@ -134,13 +134,17 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _lib = lib
-        # A/B runs only: HVK_OPTIONS="name=value,..." sets library options once at load (loudly);
-        # libhvk itself reads no environment variable
-        for item in filter(None, os.environ.get("HVK_OPTIONS", "").split(",")):
-            name, _, value = item.partition("=")
-            set_option(name.strip(), int(value))
-            print(f"[hvamd] libhvk option {name.strip()} = {int(value)} (HVK_OPTIONS)", file=sys.stderr)
     return _lib
+
+
+# the library's named options (include/hvk.h, hvk_set_option); bench.py prints options()
+LIB_OPTIONS = ("wmsa_fwd_form", "wmsa_bwd_nt", "wmsa_bwd_slice_bytes", "gemm_pp", "tile_wide", "dw_tile",
+               "gemm_xr")
+
+
+def options():
+    """{name: value} of every libhvk option (what a result line names beside options.as_dict())."""
+    return {n: get_option(n) for n in LIB_OPTIONS}
 
 
 def set_option(name, value):

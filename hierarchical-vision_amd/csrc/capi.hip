@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "hvk_common.h"
+#include "../../include/hvk.h"
 
 static thread_local char g_hvk_err[512] = "";
 
@@ -21,7 +22,7 @@ int hvk_set_error(int code, const char* fmt, ...) {
 
 const char* hvk_last_error_string(void) { return g_hvk_err; }
 
-int hvk_abi_version(void) { return 9; }
+int hvk_abi_version(void) { return HVK_ABI_VERSION; }
 
 }  // extern "C"
 
@@ -72,11 +73,17 @@ int hvk_get_option(const char* name, long long* value) {
 
 // ---- kernel timer ------------------------------------------------------------------
 namespace {
+struct TimerShape {
+  char name[48];  // "family<epi,tile>"; empty: no shape recorded
+  double mnk[3], bytes;
+};
 struct TimerRec {
   int kind;
   double work;
   hipEvent_t start, stop;
+  TimerShape shape;
 };
+TimerShape g_pending_shape{};
 std::vector<TimerRec> g_timer;  // event pool (created once, reused)
 size_t g_timer_used = 0;
 bool g_timer_on = false;
@@ -91,15 +98,26 @@ void hvk_timer_next(int kind, double work, hipEvent_t* start, hipEvent_t* stop) 
   TimerRec& r = g_timer[g_timer_used++];
   r.kind = kind;
   r.work = work;
+  r.shape = g_pending_shape;
+  g_pending_shape.name[0] = 0;
   *start = r.start;
   *stop = r.stop;
+}
+
+void hvk_timer_shape(const char* family, int epi, int tile, double m, double n, double k, double bytes) {
+  if (!g_timer_on) return;
+  snprintf(g_pending_shape.name, sizeof(g_pending_shape.name), "%s<%d,%d>", family, epi, tile);
+  g_pending_shape.mnk[0] = m;
+  g_pending_shape.mnk[1] = n;
+  g_pending_shape.mnk[2] = k;
+  g_pending_shape.bytes = bytes;
 }
 
 int hvk_kernel_timer_enable(int max_launches) {
   g_timer_used = 0;
   g_timer_on = max_launches > 0;
   while (g_timer.size() < (size_t)(max_launches > 0 ? max_launches : 0)) {
-    TimerRec r{-1, 0.0, nullptr, nullptr};
+    TimerRec r{-1, 0.0, nullptr, nullptr, {}};
     if (hipEventCreate(&r.start) != hipSuccess || hipEventCreate(&r.stop) != hipSuccess)
       return hvk_set_error(HVK_EHIP, "hvk_kernel_timer_enable: hipEventCreate failed");
     g_timer.push_back(r);
@@ -143,6 +161,18 @@ int hvk_kernel_timer_launch(int index, int* kind, double* ms, double* work) {
   *kind = r.kind;
   *ms = t;
   if (work) *work = r.work;
+  return HVK_OK;
+}
+
+int hvk_kernel_timer_launch_shape(int index, char* name, int name_cap, double* mnk, double* bytes) {
+  if (!name || name_cap < 1 || !mnk || !bytes)
+    return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_launch_shape: null pointer");
+  if (index < 0 || (size_t)index >= g_timer_used)
+    return hvk_set_error(HVK_EINVAL, "hvk_kernel_timer_launch_shape: index %d of %zu", index, g_timer_used);
+  const TimerShape& s = g_timer[index].shape;
+  snprintf(name, (size_t)name_cap, "%s", s.name);
+  for (int i = 0; i < 3; ++i) mnk[i] = s.mnk[i];
+  *bytes = s.bytes;
   return HVK_OK;
 }
 

@@ -623,6 +623,11 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   if (row_groups < 8) row_groups = 8;
   const dim3 grid(row_groups * ncb);
   const double flops = 2.0 * M * N * K;
+  // algorithmic bytes: X, W read once, Y written once; EPI 1 also writes GELU(h), EPI 2 reads h,
+  // EPI 4 writes 1/||.|| per token and q / k head (f32)
+  hvk_timer_shape("linear", EPI, BN, M, N, K,
+                  2.0 * ((double)M * K + (double)N * K + (double)M * N) +
+                      (EPI == 1 || EPI == 2 ? 2.0 * M * N : 0.0) + (EPI == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0));
   if (bias)
     HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
                        ncb, row_groups, csum, qscale);
@@ -784,6 +789,8 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
   const int need = (tiles + WAVES - 1) / WAVES;
   if (groups > need) groups = need;
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // x in; h, GELU(h), y out (the hidden tensors are written for the backward, never re-read here)
+  hvk_timer_shape("mlp_fwd", 1, WAVES, M, N1, K, 2.0 * M * (K + 2.0 * N1 + N2) + 4.0 * N1 * K);
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_fwd_kernel<WAVES>), dim3(groups),
                      dim3(64 * WAVES), LDS, st, static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w1),
                      b1, static_cast<const hvk_bf16*>(w2), b2, static_cast<hvk_bf16*>(h),
@@ -815,6 +822,8 @@ int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t,
   int groups = g_cu_count;
   const int need = (tiles + WAVES - 1) / WAVES;
   if (groups > need) groups = need;
+  // gy, h in; gh (for fc1's weight gradient), gx out
+  hvk_timer_shape("mlp_bwd", 2, WAVES, M, N1, K, 2.0 * M * (K + 2.0 * N1 + N2) + 4.0 * N1 * K);
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_bwd_kernel<WAVES>), dim3(groups),
                      dim3(64 * WAVES), LDS, static_cast<hipStream_t>(stream), static_cast<const hvk_bf16*>(gy),
                      static_cast<const hvk_bf16*>(w2t), static_cast<const hvk_bf16*>(h),

@@ -618,6 +618,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const hvk_bf16* __restr
                                                                     smem, m0, n0);
 }
 
+// algorithmic HBM bytes of one Y = X W^T launch: X, W read once, Y written once; EPI 1 also
+// writes GELU(h), EPI 2 reads h, EPI 4 writes 1/||.|| per token and q / k head (f32)
+double tile_bytes(int epi, double M, double N, double K) {
+  return 2.0 * (M * K + N * K + M * N) + (epi == 1 || epi == 2 ? 2.0 * M * N : 0.0) +
+         (epi == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0);
+}
+
 template <int EPI, int WTM, int WTN>
 int launch_pp_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                int M, int N, int K, hipStream_t st) {
@@ -630,6 +637,7 @@ int launch_pp_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16
   }
   const int mtiles = (M + BMP - 1) / BMP;
   const dim3 grid((mtiles + 7) / 8 * 8 * (N / BNP));
+  hvk_timer_shape("gemm_pp", EPI, BNP, M, N, K, tile_bytes(EPI, M, N, K));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_pp_kernel<EPI, WTM, WTN>), grid, dim3(512),
                      LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles);
   HVK_CHECK_LAUNCH("hvk_gemm_tile(pp)");
@@ -666,6 +674,7 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   const int mtiles = (M + BM - 1) / BM;
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / T::BN));
+  hvk_timer_shape("gemm_nt", EPI, T::BN, M, N, K, tile_bytes(EPI, M, N, K));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
                      T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");

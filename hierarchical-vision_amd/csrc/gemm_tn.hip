@@ -323,6 +323,11 @@ int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, 
   }
   const dim3 grid((unsigned)((p.ntiles * p.nchunk + 7) / 8 * 8));
   const double flops = 2.0 * p.nslices * TOK * N * K;  // g^T x (the fused db adds 2 M N)
+  {  // algorithmic bytes: g and x read once, dW (+ db) written once in f32 (partial slabs excluded)
+    const double M = (double)p.nslices * TOK;
+    hvk_timer_shape(GX ? "dw_gelu_x" : "dw", with_db ? 1 : 0, C::TN, M, N, K,
+                    2.0 * M * (N + K) + 4.0 * N * K + (with_db ? 4.0 * N : 0.0));
+  }
   if (with_db)
     HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, true, GX>), grid, dim3(C::THREADS),
                        C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);

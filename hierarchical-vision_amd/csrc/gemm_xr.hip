@@ -355,6 +355,8 @@ int launch_(const hvk_xr::Args& a, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
+  hvk_timer_shape("gemm_xr", EPI, IL, a.M, a.N, a.K,
+                  2.0 * ((double)a.M * a.K + (double)a.N * a.K + (double)a.M * a.N * (EPI == 1 || EPI == 2 ? 2 : 1)));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * a.M * a.N * a.K, (gemm_xr_kernel<EPI, IL>), dim3(256), dim3(512), LDS,
                      st, a);
   HVK_CHECK_LAUNCH("hvk_gemm_xr");

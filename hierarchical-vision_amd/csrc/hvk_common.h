@@ -62,6 +62,10 @@ extern "C" {
 // null pair: not timed; work = the launch's algorithmic flops (or bytes), summed by read
 __attribute__((visibility("hidden"))) void hvk_timer_next(int kind, double work, hipEvent_t* start,
                                                      hipEvent_t* stop);
+// the shape of the NEXT timed GEMM launch (kernel family, epilogue, tile variant, M N K and its
+// algorithmic HBM bytes), taken by hvk_timer_next: bench.py's per-shape binding-roof table
+__attribute__((visibility("hidden"))) void hvk_timer_shape(const char* family, int epi, int tile, double m,
+                                                      double n, double k, double bytes);
 #ifdef __cplusplus
 }
 #endif

@@ -3,11 +3,15 @@ the backward pass (the one hot-path collective; the reference
 gets it implicitly from composer's DDP wrapper, main.py:104-124).
 
 Design for MI355X:
-* Gradients live in a few large flat f32 buffers ("buckets"), one per ~`bucket_mb`
-  of parameters in reverse registration order (= roughly backward order), the first
-  (last layers: head, stage 3) only ~`first_mb` so the first all-reduce starts early;
-  after the exchange every ``param.grad`` is a view into its bucket (the optimizer and
-  the clip read the buckets, no pack / unpack copy).
+* Gradients live in a few large flat f32 buffers ("buckets") in reverse registration order
+  (= roughly backward order): the first closes as soon as it holds ``first_mb`` (so it is the
+  head's gradients -- the first ready -- even when one of them alone is larger: the 30.7 MB
+  10 000-leaf HXE head weight), the middle ones hold up to ``bucket_mb`` each, and the LAST holds
+  only the earliest-registered ``last_mb`` (patch embedding, stage 0, ...): its all-reduce can
+  start only when the backward's final gradient lands, so it is the exchange's exposed tail and
+  is kept small; every larger bucket is enqueued while the backward still runs.  After the
+  exchange every ``param.grad`` is a view into its bucket (the optimizer and the clip read the
+  buckets, no pack / unpack copy).
 * Between steps ``param.grad`` is None, so autograd hands each fresh weight gradient over
   without a ``grad += new`` pass (and the buckets need no per-step zero_); the
   post-accumulate-grad hook copies it into its bucket view (one read + one write of the
@@ -29,7 +33,7 @@ import torch.distributed as dist
 
 class GradientBuckets:
     def __init__(self, module: torch.nn.Module, bucket_mb: float = 64.0, process_group=None,
-                 first_mb: float = 8.0, force: bool = False):
+                 first_mb: float = 8.0, force: bool = False, last_mb: float = 4.0):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         params = [p for p in module.parameters() if p.requires_grad]
@@ -48,25 +52,54 @@ class GradientBuckets:
         self._hooks = []
         if not self.enabled:  # single rank: nothing to exchange, let autograd own .grad
             return
-        limit = int(bucket_mb * 1024 * 1024 / 4)
-        first = int(min(first_mb, bucket_mb) * 1024 * 1024 / 4)
         self.buckets = []  # list of (flat buffer, [params])
         self._view = {}    # param -> its view in the bucket
-        cur, size = [], 0
-        for p in reversed(params):
-            if cur and size + p.numel() > (first if not self.buckets else limit):
-                self.buckets.append(self._make(cur, size))
-                cur, size = [], 0
-            cur.append(p)
-            size += p.numel()
-        if cur:
-            self.buckets.append(self._make(cur, size))
+        for group in self.plan([p.numel() for p in params], bucket_mb, first_mb, last_mb):
+            ps = [params[i] for i in group]
+            self.buckets.append(self._make(ps, sum(p.numel() for p in ps)))
         self._pending = [0] * len(self.buckets)
         self._works = [None] * len(self.buckets)
         for bi, (_, ps) in enumerate(self.buckets):
             for p in ps:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(bi)))
         self.reset()
+
+    @staticmethod
+    def plan(numels, bucket_mb=64.0, first_mb=8.0, last_mb=4.0):
+        """Bucket assignment for parameters of `numels` elements (f32) in registration order:
+        a list of buckets, each a list of parameter indices, in exchange (= backward) order.
+        The tail -- the earliest-registered parameters, at least one, up to min(last_mb,
+        bucket_mb) -- is the last bucket; the rest in reverse order: the first bucket closes
+        once it reaches first_mb (a parameter larger than that joins it rather than waiting
+        behind it), later ones are cut before they would exceed bucket_mb."""
+        mb = 1024 * 1024 / 4
+        limit, first = int(bucket_mb * mb), int(min(first_mb, bucket_mb) * mb)
+        tail_cap = int(min(last_mb, bucket_mb) * mb)
+        n_tail, t = 1, numels[0] if numels else 0
+        while n_tail < len(numels) - 1 and t + numels[n_tail] <= tail_cap:
+            t += numels[n_tail]
+            n_tail += 1
+        if len(numels) <= 1:
+            n_tail = len(numels)
+        out, cur, size = [], [], 0
+        for i in range(len(numels) - 1, n_tail - 1, -1):
+            if not out:  # first bucket: close once it has first_mb
+                cur.append(i)
+                size += numels[i]
+                if size >= first:
+                    out.append(cur)
+                    cur, size = [], 0
+                continue
+            if cur and size + numels[i] > limit:
+                out.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += numels[i]
+        if cur:
+            out.append(cur)
+        if n_tail:
+            out.append(list(range(n_tail - 1, -1, -1)))
+        return out
 
     def _make(self, params, n):
         dev = params[0].device

@@ -5,13 +5,13 @@ current stream; tensors are plumbing (PyTorch owns the memory).  There is no
 eager/CPU fallback: a CPU tensor or a missing library raises.
 """
 import ctypes
-import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _lib
 from ._lib import call, ptr, stream
+from .options import OPTIONS
 
 
 TIMER_WMSA, TIMER_GEMM, TIMER_ALL = 0x3, 0xC, 0xF  # kind masks (include/hvk.h)
@@ -33,6 +33,24 @@ def kernel_timer_launches(kind):
     while lib.hvk_kernel_timer_launch(i, ctypes.byref(k), ctypes.byref(t), ctypes.byref(w)) == 0:
         if k.value == kind:
             out.append(t.value)
+        i += 1
+    return out
+
+
+def kernel_timer_shapes(kinds=(2, 3)):
+    """Every timed GEMM launch since kernel_timer_start (call before kernel_timer_stop), in
+    launch order: dicts with the kernel family name, kind, M, N, K, algorithmic bytes and flops
+    (2 M N K; 4 M N1 K for the fused MLP kernels, as the library records) and duration (ms)."""
+    out, i = [], 0
+    k, t, w = ctypes.c_int(0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+    name = ctypes.create_string_buffer(64)
+    mnk, nb = (ctypes.c_double * 3)(), ctypes.c_double(0.0)
+    lib = _lib.load()
+    while lib.hvk_kernel_timer_launch(i, ctypes.byref(k), ctypes.byref(t), ctypes.byref(w)) == 0:
+        if k.value in kinds:
+            call("hvk_kernel_timer_launch_shape", i, name, 64, mnk, ctypes.byref(nb))
+            out.append({"kernel": name.value.decode(), "kind": k.value, "M": int(mnk[0]), "N": int(mnk[1]),
+                        "K": int(mnk[2]), "bytes": nb.value, "flops": w.value, "ms": t.value})
         i += 1
     return out
 
@@ -109,13 +127,12 @@ class _WeightCopies:
 
 
 _WCOPIES = _WeightCopies()
-_PREPARE = os.environ.get("HVK_PREPARE_WEIGHTS", "1") != "0"  # 0: per-call casts (A/B runs)
 
 
 def prepare_weights(weights):
     """Refresh the bf16 copies (+ transposes) of `weights` (f32 [N, K] masters) in one launch;
     the Linear Functions below then use them for this step."""
-    if weights and _PREPARE:
+    if weights and OPTIONS.prepare_weights:
         _WCOPIES.prepare(weights)
 
 
@@ -142,17 +159,13 @@ def _split_k_chunks(rows):
     return nc
 
 
-# 1: keep only h and recompute GELU(h) in fc2 (off: measured slower)
-_GELU_RECOMPUTE = os.environ.get("HVK_GELU_RECOMPUTE", "0") == "1"
-
-
 def _gelu_recompute(M, K, N1, N2):
-    """With HVK_GELU_RECOMPUTE=1, MlpFn keeps only h = fc1(x) and recomputes GELU(h) inside
+    """With options.gelu_recompute, MlpFn keeps only h = fc1(x) and recomputes GELU(h) inside
     fc2's forward and weight gradient where both kernels are built (stage 0: K 96, N1 384,
     N2 96).  Bit-identical results; off by default: on MI355X the recompute costs fc2 +80 µs
     and its weight gradient +217 µs against the 233 µs the y write saves."""
     lib = _lib.load()
-    return (_GELU_RECOMPUTE and _linear_native(M, K, N1) and lib.hvk_linear_gelu_in_supported(M, N1, N2)
+    return (OPTIONS.gelu_recompute and _linear_native(M, K, N1) and lib.hvk_linear_gelu_in_supported(M, N1, N2)
             and lib.hvk_weight_grad_gelu_x_supported(M, N2, N1))
 
 
@@ -214,11 +227,6 @@ def _linear_native(M, K, N):
     return ok and M > 0
 
 
-_TILE_ROUTE = int(os.environ.get("HVK_TILE_ROUTE", "1"))
-_TILE_S3 = int(os.environ.get("HVK_TILE_S3", "1"))
-_TILE_S1 = int(os.environ.get("HVK_TILE_S1", "1"))
-
-
 def _tile_ok(M, K, N):
     """libhvk's tiled MFMA GEMM (hvk_gemm_fwd) where it measured faster than the library GEMM
     (tools/bench_gemm.py): the stage-2 shapes (K <= 1536, fc2 forward and fc1 input gradient
@@ -226,13 +234,9 @@ def _tile_ok(M, K, N):
     stage-2 PatchMerging) with 192 | N, on 128 x 192 tiles."""
     if K % 64 or M <= 0:
         return False
-    if _TILE_ROUTE == 0:  # the earlier routing (A/B experiments): stage 2 with K <= 1152
-        return not N % 128 and ((M >= 32768 and K <= 1152) or (K == 768 and N == 768))
     if N % 128:  # the 128 x 192 tile: stage-1 qkv / proj / fc2 forward, qkv / fc1 input grads
-        if not _TILE_S1:  # the narrower rule (A/B runs)
-            return N == 192 and K in (576, 768) and M >= 32768
         return N % 192 == 0 and K >= 192 and M >= 32768
-    if _TILE_S3 and M >= 8192 and N % 192 == 0:  # stage 3 and its PatchMerging (128 x 192 tiles)
+    if M >= 8192 and N % 192 == 0:  # stage 3 and its PatchMerging (128 x 192 tiles)
         return True
     return (M >= 32768 and K <= 1536) or (K == 768 and N == 768)
 
@@ -242,9 +246,10 @@ def _native_nt(M, K, N):
     return _tile_ok(M, K, N) or _linear_native(M, K, N)
 
 
-# fc1 + GELU widths on the skinny kernel (stage 0 outside the fused MLP; stage 1 unless
-# HVK_S1_GELU_TILE=1 routes it to the tiled EPI 1 kernel, A/B runs)
-_GELU_SKINNY_K = (96,) if os.environ.get("HVK_S1_GELU_TILE", "0") == "1" else (96, 192)
+def _gelu_skinny_k():
+    """fc1 + GELU widths on the skinny kernel (stage 0 outside the fused MLP; stage 1 unless
+    options.s1_gelu_tile routes it to the tiled EPI 1 kernel)."""
+    return (96,) if OPTIONS.s1_gelu_tile else (96, 192)
 
 
 def gelu_fwd(x2, wb, bias):
@@ -253,7 +258,7 @@ def gelu_fwd(x2, wb, bias):
     M, K = x2.shape
     N = wb.shape[0]
     lib = _lib.load()
-    if (K in _GELU_SKINNY_K or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N):
+    if (K in _gelu_skinny_k() or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N):
         fn = "hvk_linear_gelu_fwd"
     elif _tile_ok(M, K, N):
         fn = "hvk_gemm_gelu_fwd"
@@ -265,12 +270,13 @@ def gelu_fwd(x2, wb, bias):
     return h, y
 
 
-# SwinV2-B's stage 0-1 widths (K = 128 / 256): the skinny kernel before the tiled one
-_SKINNY_FIRST = {128, 256} if os.environ.get("HVK_SKINNY_B", "1") != "0" else set()
+def _skinny_first_k():
+    """SwinV2-B's stage 0-1 widths (K = 128 / 256): the skinny kernel before the tiled one."""
+    return (128, 256) if OPTIONS.skinny_b else ()
 
 
 def _skinny_first(M, K, N):
-    return K in _SKINNY_FIRST and _linear_native(M, K, N)
+    return K in _skinny_first_k() and _linear_native(M, K, N)
 
 
 def mm_nt(x2, wb, bias=None):
@@ -388,12 +394,40 @@ class LinearQkvFn(torch.autograd.Function):
 
 def linear_qkv(x, weight, bias, scale):
     """The qkv Linear with q, k normalised and q pre-scaled by the attention's logit scale
-    (`scale` [nH], detached here: its gradient comes from window_attention_core)."""
-    return LinearQkvFn.apply(x, weight, bias, scale)
+    (`scale` [nH], detached here: its gradient comes from window_attention_core).
+
+    Gradient contract (non-standard): the returned qkv^ must be consumed ONLY by
+    window_attention_core(..., rn=rn), whose backward returns the gradient with respect to the
+    UN-normalised qkv -- the one LinearQkvFn.backward expects.  Any other consumer would get
+    wrong gradients, so the output is tagged and window_attention_core refuses an rn paired with
+    an untagged qkv."""
+    y, rn = LinearQkvFn.apply(x, weight, bias, scale)
+    y._hvk_qk_normed = True
+    return y, rn
 
 
 # --------------------------------------------------------------------------- classifier head
 _HEAD_WS = {}
+_HEAD_W = {}  # device -> (key, concatenated bf16 tier weights): rebuilt only when a weight changes
+
+
+def _head_weight(ws, K, Np, device):
+    """The tiers' bf16 weights concatenated (and zero-padded to Np rows) once per optimizer
+    update, keyed on the f32 masters' storage and version counters, instead of a fresh
+    [Np, K] copy every forward (15 MB for a 10 000-class head)."""
+    if len(ws) == 1 and ws[0].shape[0] == Np:
+        return _bf16_weight(ws[0])[0]
+    key = tuple((w.data_ptr(), w._version, tuple(w.shape)) for w in ws) + (Np, K)
+    c = _HEAD_W.get(device)
+    if c is not None and c[0] == key:
+        return c[1]
+    buf = torch.zeros((Np, K), device=device, dtype=torch.bfloat16)
+    off = 0
+    for w in ws:
+        buf[off:off + w.shape[0]].copy_(_bf16_weight(w)[0])
+        off += w.shape[0]
+    _HEAD_W[device] = (key, buf)
+    return buf
 
 
 class HeadFn(torch.autograd.Function):
@@ -410,10 +444,7 @@ class HeadFn(torch.autograd.Function):
         sizes = [w.shape[0] for w in ws]
         N = sum(sizes)
         Np = (N + 7) // 8 * 8
-        wcat = [_bf16_weight(w)[0] for w in ws]
-        if Np != N:
-            wcat.append(torch.zeros((Np - N, K), device=xb.device, dtype=torch.bfloat16))
-        wcat = wcat[0] if len(wcat) == 1 else torch.cat(wcat, dim=0)
+        wcat = _head_weight(ws, K, Np, xb.device)
         has_b = all(b is not None for b in bs) and len(bs) == n_w
         bcat = None
         if has_b:
@@ -538,11 +569,6 @@ def _wmsa_workspace(device, nbytes):
     return ws
 
 
-# windows 12 / 16 / 24: the forward keeps the row constants and the backward skips its
-# row-statistics pass (0: recompute them, A/B runs)
-_WMSA_LARGE_LSE = os.environ.get("HVK_WMSA_LARGE_LSE", "1") != "0"
-
-
 class WindowAttentionCore(torch.autograd.Function):
     """Shifted-window cosine attention core on un-partitioned tokens.
 
@@ -572,7 +598,9 @@ class WindowAttentionCore(torch.autograd.Function):
                  num_heads, window, shift, stream())
             ctx.save_for_backward(qkv, bias_table, scale, rn)
             return out
-        keep = _WMSA_LARGE_LSE and window > 8
+        # windows 12 / 16 / 24: the forward keeps the row constants and the backward skips its
+        # row-statistics pass (options.wmsa_large_lse False: recompute them)
+        keep = OPTIONS.wmsa_large_lse and window > 8
         lse = torch.empty((B, L, num_heads), device=qkv.device, dtype=torch.float32) if keep else None
         call("hvk_wmsa_fwd", ptr(qkv), ptr(out), ptr(lse), ptr(bias_table), ptr(scale), B, H, W, C,
              num_heads, window, shift, stream())
@@ -623,6 +651,9 @@ class WindowAttentionCore(torch.autograd.Function):
 def window_attention_core(qkv, bias_table, scale, H, W, num_heads, window, shift, q_bias=None, rn=None):
     """rn given: qkv holds (q^, k^, v) from linear_qkv (windows <= 8) and the gradient returned
     for it is the one with respect to the un-normalised qkv."""
+    if rn is not None and not getattr(qkv, "_hvk_qk_normed", False):
+        raise ValueError("window_attention_core(rn=...) takes the qkv^ returned by linear_qkv itself "
+                         "(its backward returns the gradient of the un-normalised qkv)")
     return WindowAttentionCore.apply(qkv, q_bias, bias_table, scale, H, W, num_heads, window,
                                      shift, rn)
 
@@ -909,13 +940,10 @@ def linear_gelu(x, weight, bias):
     """GELU(F.linear(x, weight, bias)): fused kernel where built, else GEMM + activation kernel."""
     N, K = weight.shape
     M = x.numel() // K
-    if bias is not None and (((K in (96, 192) or K in _SKINNY_FIRST)
+    if bias is not None and (((K in (96, 192) or K in _skinny_first_k())
                               and _lib.load().hvk_linear_gelu_supported(M, K, N)) or _tile_ok(M, K, N)):
         return LinearGelu.apply(x, weight, bias)
     return bias_gelu(linear(x, weight), bias)
-
-
-_MLP_FUSED = os.environ.get("HVK_MLP_FUSED", "1") != "0"  # 0: fc1+GELU and fc2 as two launches (A/B)
 
 
 class MlpFn(torch.autograd.Function):
@@ -944,7 +972,7 @@ class MlpFn(torch.autograd.Function):
             call("hvk_linear_gelu_in_fwd", ptr(h), ptr(w2b), ptr(b) if b is not None else None, ptr(y), M,
                  N1, N2, stream())
             ctx.save_for_backward(xb, w1b, w2b, h)
-        elif _MLP_FUSED and _lib.load().hvk_mlp_fwd_supported(M, K, N1, N2):
+        elif OPTIONS.mlp_fused and _lib.load().hvk_mlp_fwd_supported(M, K, N1, N2):
             # stage-0 width: fc1 + GELU + fc2 in one kernel (no re-read of GELU(h))
             h = torch.empty((M, N1), device=x2.device, dtype=torch.bfloat16)
             y1 = torch.empty_like(h)
@@ -976,7 +1004,7 @@ class MlpFn(torch.autograd.Function):
             dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
         gh = torch.empty_like(h)
         w2t = _bf16_t(w2b, ctx.wts[1])
-        if (_MLP_FUSED and ctx.needs_input_grad[0] and not ctx.recompute
+        if (OPTIONS.mlp_fused and ctx.needs_input_grad[0] and not ctx.recompute
                 and _lib.load().hvk_mlp_bwd_supported(M, N2, N1, K)):
             # stage-0 width: fc2's input gradient through GELU' and fc1's input gradient in one
             # kernel (gh stored for fc1's weight gradient, not re-read for gx)
@@ -985,7 +1013,7 @@ class MlpFn(torch.autograd.Function):
                  M, N2, N1, K, stream())
             dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
             return gx.reshape(xb.shape), dw1, db1, dw2, db2
-        if _tile_ok(M, N2, N1) and not (N2 in _SKINNY_FIRST and
+        if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
                                          _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
             call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
         else:
@@ -1005,7 +1033,7 @@ def mlp(x, w1, b1, w2, b2=None):
     N1, K = w1.shape
     M = x.numel() // K
     lib = _lib.load()
-    if (b1 is not None and (((K in (96, 192) or K in _SKINNY_FIRST) and lib.hvk_linear_gelu_supported(M, K, N1))
+    if (b1 is not None and (((K in (96, 192) or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N1))
                             or _tile_ok(M, K, N1))
             and (lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1) or _tile_ok(M, w2.shape[0], N1))):
         return MlpFn.apply(x, w1, b1, w2, b2)

@@ -4,9 +4,9 @@ no-decay rule and multi-tensor (foreach) update kernels.
 Quirk kept from the reference: build_optimizer is handed the Composer wrapper,
 which has no `no_weight_decay`, so the skip set is always empty and 3-D
 `logit_scale` is decayed (optim.py:9-14, 53)."""
-import os
-
 import torch
+
+from .options import OPTIONS
 
 
 def set_weight_decay(model, skip_list=()):
@@ -58,7 +58,7 @@ class DecoupledSGDW(torch.optim.Optimizer):
         return self._fused_eligible() and mine == {id(p) for p in params}
 
     def _fused_eligible(self):
-        if os.environ.get("HVK_FUSED_OPTIM", "1") == "0":  # A/B runs: the foreach path
+        if not OPTIONS.fused_optim:  # A/B runs: the foreach path
             return False
         gs = self.param_groups
         if not gs or any(g["nesterov"] != gs[0]["nesterov"] or g["momentum"] != gs[0]["momentum"]

@@ -1,0 +1,86 @@
+"""Host-side routing switches of the product path, as ONE explicit object.
+
+Every switch here picks between two implementations of the same op that are pinned to each
+other by a test (the alternative form exists for A/B measurements and for those tests).  They
+are plain attributes of `OPTIONS`, changed only through `set()` / `override()` -- no module of
+the package reads the process environment (HVK_LIB_PATH, the library's location, aside) -- and
+bench.py prints `as_dict()` into its JSON line, so a result always names the forms it ran.
+
+The library-side forms (tile widths, the ring W-MSA forward, ...) are libhvk options
+(`_lib.set_option`, include/hvk.h); `_lib.options()` reads them back the same way.
+"""
+import contextlib
+import dataclasses
+
+
+@dataclasses.dataclass
+class HostOptions:
+    # bf16 copies (+ transposes) of every Linear weight made by one launch per step
+    # (ops.prepare_weights); False: a cast per Linear call
+    prepare_weights: bool = True
+    # windows <= 8: q / k normalised (and q pre-scaled) in the qkv GEMM's epilogue
+    # (swinv2.py:229-231); False: raw qkv, the W-MSA kernels normalise
+    qk_epilogue: bool = True
+    # a block's attention biases + CPB table + logit scale as one launch (ops.block_tables)
+    block_tables: bool = True
+    # classifier / multitask head on libhvk's head GEMM (ops.head_linear)
+    head_gemm: bool = True
+    # final LayerNorm + token mean pool as one kernel each way (ops.norm_pool)
+    norm_pool: bool = True
+    # the stage-0 MLP forward / input-gradient chain as one kernel each (hvk_mlp_fwd / _bwd)
+    mlp_fused: bool = True
+    # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
+    fused_optim: bool = True
+    # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward
+    wmsa_large_lse: bool = True
+    # SwinV2-B stage 0-1 widths (K = 128 / 256) on the skinny kernel ahead of the tiled one
+    skinny_b: bool = True
+    # stage-1 fc1 + GELU on the tiled EPI-1 kernel instead of the skinny one (measured -0.1 %)
+    s1_gelu_tile: bool = False
+    # keep only fc1's h at stage 0 and recompute GELU(h) where consumed (measured -0.4 %)
+    gelu_recompute: bool = False
+
+
+OPTIONS = HostOptions()
+_FIELDS = {f.name: f.type for f in dataclasses.fields(HostOptions)}
+
+
+def set(**kw):  # noqa: A001 -- options.set(name=value)
+    """Set host options by name; returns the previous values (a dict).  Unknown names raise."""
+    prev = {}
+    for k, v in kw.items():
+        if k not in _FIELDS:
+            raise KeyError(f"unknown host option {k!r} (known: {sorted(_FIELDS)})")
+        prev[k] = getattr(OPTIONS, k)
+        setattr(OPTIONS, k, bool(v) if _FIELDS[k] in (bool, "bool") else v)
+    return prev
+
+
+@contextlib.contextmanager
+def override(**kw):
+    """with options.override(qk_epilogue=False): ... -- restores the previous values."""
+    prev = set(**kw)
+    try:
+        yield OPTIONS
+    finally:
+        set(**prev)
+
+
+def parse(text):
+    """'name=value' -> {name: value} with value int / bool ('0', '1', 'true', 'false')."""
+    name, _, value = text.partition("=")
+    name, value = name.strip(), value.strip().lower()
+    if name not in _FIELDS:
+        raise KeyError(f"unknown host option {name!r} (known: {sorted(_FIELDS)})")
+    v = {"true": 1, "false": 0}.get(value)
+    return {name: int(value) if v is None else v}
+
+
+def as_dict():
+    return dataclasses.asdict(OPTIONS)
+
+
+def non_default():
+    """The options that differ from the defaults (what a result line must name)."""
+    d = HostOptions()
+    return {k: v for k, v in as_dict().items() if getattr(d, k) != v}

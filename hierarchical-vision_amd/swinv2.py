@@ -22,7 +22,6 @@ block is re-planned around the hardware:
   the classifier / multitask heads (M = batch) stay on hipBLASLt via torch.
 """
 import dataclasses
-import os
 import re
 from typing import NamedTuple
 
@@ -33,6 +32,7 @@ import torch.nn.functional as F
 import torch.utils.checkpoint as checkpoint
 
 from . import ops
+from .options import OPTIONS
 from .hierarchy import MultitaskHead  # noqa: F401  (re-exported like swinv2.py:12-40)
 
 
@@ -138,6 +138,12 @@ class Mlp(nn.Module):
         return self.drop(ops.linear_gelu(x, self.fc1.weight, self.fc1.bias))
 
 
+class ProjFoldTables(tuple):
+    """block_tables()'s fused result (qkv GEMM bias, proj bias, CPB table, logit scale): its proj
+    bias holds W_proj v_bias with W_proj detached, so the proj Linear adds that share of
+    d proj.weight in its weight-gradient kernel (ops.linear(..., xshift=v_bias))."""
+
+
 class WindowAttention(nn.Module):
     """W-MSA / SW-MSA with continuous (log-spaced CPB) relative-position bias
     (swinv2.py:105-264).  Parameters and buffers match the reference."""
@@ -226,18 +232,20 @@ class WindowAttention(nn.Module):
 
     def block_tables(self):
         """(qkv GEMM bias, proj bias, CPB table, logit scale) = gemm_biases() + cpb_tables(),
-        on the GPU as one fused launch (ops.block_tables) when both fused forms apply."""
+        on the GPU as one fused launch (ops.block_tables) when both fused forms apply.  The
+        fused form returns a `ProjFoldTables`: its proj bias took W_proj detached, so the proj
+        Linear that consumes it must add the W_proj v_bias share of the weight gradient itself
+        (forward_tokens keys that on the returned object, never on state left behind)."""
         l1, l2 = self.cpb_mlp[0], self.cpb_mlp[2]
-        if (self.v_bias is not None and self.v_bias.is_cuda and _FUSED_TABLES
+        if (self.v_bias is not None and self.v_bias.is_cuda and OPTIONS.block_tables
                 and isinstance(self.cpb_mlp[1], nn.ReLU) and l1.bias is not None and l2.bias is None
                 and l1.out_features == 512 and self.num_heads <= 32):
             # W_proj enters the folded bias detached: forward_tokens' proj Linear takes the
             # W_proj v_bias share of its weight gradient (xshift = v_bias, one fused kernel)
-            self._proj_fold = True  # a plain bool (a Parameter attribute would register a parameter)
-            return ops.block_tables(self.v_bias, self.proj.bias, self.proj.weight.detach(),
-                                    self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias,
-                                    l2.weight, self.logit_scale, self.q_bias, self._logit_clamp)
-        self._proj_fold = False
+            return ProjFoldTables(ops.block_tables(
+                self.v_bias, self.proj.bias, self.proj.weight.detach(),
+                self.relative_coords_table.reshape(-1, 2), l1.weight, l1.bias, l2.weight,
+                self.logit_scale, self.q_bias, self._logit_clamp))
         return self.gemm_biases() + self.cpb_tables()
 
     def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None):
@@ -248,15 +256,19 @@ class WindowAttention(nn.Module):
             biases = self.block_tables()
         qkv_b, proj_b = biases[:2]
         table, scale = biases[2:] if len(biases) == 4 else self.cpb_tables()
-        if _QK_EPILOGUE and self.window_size[0] <= 8:
+        if OPTIONS.qk_epilogue and self.window_size[0] <= 8:
             # q / k normalisation (swinv2.py:229) in the qkv GEMM's epilogue
             qkv, rn = ops.linear_qkv(x, self.qkv.weight, qkv_b, scale)
         else:
             qkv, rn = ops.linear(x, self.qkv.weight, qkv_b), None
         o = ops.window_attention_core(qkv, table, scale, H, W, self.num_heads,
                                       self.window_size[0], shift, q_bias=self.q_bias, rn=rn)
+        # the v_bias share of d proj.weight: from this Linear's weight-gradient kernel exactly when
+        # the proj bias came from the fused tables (W_proj detached there); gemm_biases() and the
+        # unfused tables route it through autograd already
+        fold = isinstance(biases, ProjFoldTables)
         return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None,
-                                         xshift=self.v_bias if getattr(self, "_proj_fold", False) else None))
+                                         xshift=self.v_bias if fold else None))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -505,19 +517,11 @@ class PatchEmbed(nn.Module):
         return f + (Ho * Wo * self.embed_dim if self.norm is not None else 0)
 
 
-_FUSED_TABLES = os.environ.get("HVK_BLOCK_TABLES", "1") != "0"  # 0: separate launches (A/B runs)
-# windows <= 8: q / k normalised in the qkv GEMM's epilogue, the W-MSA kernels take q^, k^ (and
-# the backward 1/||q||, 1/||k||) as they are (0: raw qkv, the kernels normalise; A/B runs)
-_QK_EPILOGUE = os.environ.get("HVK_QK_EPILOGUE", "1") != "0"
-# the classifier / multitask head on libhvk's head GEMMs (0: ops.linear / the library GEMM, A/B runs)
-_HEAD_GEMM = os.environ.get("HVK_HEAD_GEMM", "1") != "0"
-
-
 def _lib_ln_pool_ok(C):
-    """The fused final-norm + pool kernel is built for C (HVK_NORM_POOL=0: the torch form, for
-    A/B runs)."""
+    """The fused final-norm + pool kernel is built for C (options.norm_pool False: the torch
+    form)."""
     from . import _lib
-    return os.environ.get("HVK_NORM_POOL", "1") != "0" and bool(_lib.load().hvk_ln_pool_supported(C))
+    return OPTIONS.norm_pool and bool(_lib.load().hvk_ln_pool_supported(C))
 
 
 class SwinTransformerV2(nn.Module):
@@ -651,7 +655,7 @@ class SwinTransformerV2(nn.Module):
         """The classifier: a single Linear runs as ops.linear under autocast (the step's
         prepared bf16 weight, f32 dW straight from the GEMM, no per-call casts)."""
         if isinstance(self.head, nn.Linear) and x.is_cuda and torch.is_autocast_enabled():
-            if _HEAD_GEMM and ops.head_supported(x, [self.head.weight]):
+            if OPTIONS.head_gemm and ops.head_supported(x, [self.head.weight]):
                 return ops.head_linear(x, [self.head.weight], [self.head.bias])[0]
             return ops.linear(x, self.head.weight, self.head.bias)
         return self.head(x)

@@ -22,6 +22,9 @@
 extern "C" {
 #endif
 
+/* the C ABI this header describes; hvk_abi_version() returns it (bindings check it at load) */
+#define HVK_ABI_VERSION 10
+
 #define HVK_OK 0
 #define HVK_EINVAL 1
 #define HVK_EUNSUPPORTED 2
@@ -65,6 +68,12 @@ int hvk_kernel_timer_read_work(int kind, double* total_ms, int* launches, double
 /* the index-th timed launch since hvk_kernel_timer_enable, in launch order: its kind, duration
  * and the work the library recorded for it (bench.py's per-stage W-MSA breakdown) */
 int hvk_kernel_timer_launch(int index, int* kind, double* ms, double* work);
+/* the same launch's shape, for the GEMM kinds (2, 3): name = "family<epilogue,tile>" (the kernel
+ * family, e.g. gemm_nt / linear / mlp_fwd / dw, its epilogue and tile variant; "" for launches
+ * that recorded none), mnk[3] = M, N, K, bytes = its algorithmic HBM bytes (operands read once,
+ * outputs written once: bench.py's per-shape binding roof max(flops / MFMA peak, bytes / HBM peak)).
+ * ABI 10. */
+int hvk_kernel_timer_launch_shape(int index, char* name, int name_cap, double* mnk, double* bytes);
 
 /* ---- Shifted-window cosine attention core ------------------------------------------
  * Replaces swinv2.py:399-412 (roll + window_partition), 221-261 (WindowAttention core:

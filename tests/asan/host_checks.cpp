@@ -24,7 +24,7 @@ static int g_fail = 0;
 static void* const P = reinterpret_cast<void*>(0x1000);
 
 int main() {
-  EXPECT(hvk_abi_version() == 9);
+  EXPECT(hvk_abi_version() == HVK_ABI_VERSION);
 
   // options: unknown names and out-of-range values refused, set/get round trip
   long long prev = -7, v = -7;

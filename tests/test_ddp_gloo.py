@@ -71,9 +71,15 @@ def _worker_views(rank, world, port, out):
     from hvamd.ddp import GradientBuckets
     net = _net()
     net.unused = torch.nn.Parameter(torch.ones(5))
-    buckets = GradientBuckets(net, bucket_mb=0.004, first_mb=0.0005)
+    buckets = GradientBuckets(net, bucket_mb=0.004, first_mb=0.0005, last_mb=0.0025)
     sizes = [b[0].numel() for b in buckets.buckets]
-    res = {"first_small": sizes[0] <= 0.0005 * 2 ** 18 + 32 * 32 and sizes[0] < max(sizes)}
+    head_w = net[4].weight  # the last layer's weight: ready first in the backward
+    bucket_of = {id(p): i for i, (_, ps) in enumerate(buckets.buckets) for p in ps}
+    res = {"first_small": sizes[0] <= 0.0005 * 2 ** 18 + 32 * 32 and sizes[0] < max(sizes),
+           # the head weight rides in the FIRST bucket (it once waited in bucket 1 behind a
+           # 40 KB head-bias bucket), the first-registered Linear in the small LAST one
+           "head_weight_first_bucket": bucket_of[id(head_w)] == 0,
+           "embed_last_bucket": bucket_of[id(net[0].weight)] == len(sizes) - 1 and sizes[-1] <= 0.0025 * 2 ** 18}
     x, y = _data()
     res["none_before"] = all(p.grad is None for p in net.parameters())
     ok_views, unused_zero = True, True
@@ -91,6 +97,26 @@ def _worker_views(rank, world, port, out):
     res["unused_zero"] = unused_zero
     out[rank] = res
     dist.destroy_process_group()
+
+
+def test_bucket_plan_swinv2t_hxe_sizes():
+    """The bucket plan on SwinV2-T + a 10 000-leaf HXE head's real parameter sizes (built on
+    the CPU): the head weight (30.7 MB, larger than first_mb) forms the first bucket
+    with the head bias, every middle bucket stays <= 64 MB, and the last bucket -- the exposed
+    tail after the backward -- holds <= 4 MB of the earliest layers."""
+    from hvamd.ddp import GradientBuckets
+    from hvamd.swinv2 import SwinTransformerV2
+    m = SwinTransformerV2(num_classes=10000)
+    names = [n for n, p in m.named_parameters() if p.requires_grad]
+    numels = [p.numel() for p in m.parameters() if p.requires_grad]
+    plan = GradientBuckets.plan(numels)
+    mb = [4 * sum(numels[i] for i in b) / 2 ** 20 for b in plan]
+    assert sorted(i for b in plan for i in b) == list(range(len(numels)))
+    assert names.index("head.weight") in plan[0] and names.index("head.bias") in plan[0]
+    assert 8 <= mb[0] <= 40
+    assert all(x <= 64 for x in mb[1:-1])
+    assert mb[-1] <= 4 and names.index("patch_embed.proj.weight") in plan[-1]
+    assert len(plan) >= 4
 
 
 def test_bucket_views_unused_params_small_first_bucket():

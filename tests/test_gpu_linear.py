@@ -87,7 +87,7 @@ def test_mlp_gelu_recompute_bit_identical(monkeypatch, with_b2):
     gy = torch.randn(M, C, device="cuda").bfloat16()
     res = {}
     for rec in (True, False):
-        monkeypatch.setattr(ops, "_GELU_RECOMPUTE", rec)
+        monkeypatch.setattr(ops.OPTIONS, "gelu_recompute", rec)
         assert ops._gelu_recompute(M, C, 4 * C, C) == rec
         ps = [t.clone().requires_grad_(True) if t is not None else None for t in (x0, w1, b1, w2, b2)]
         y = ops.MlpFn.apply(*ps)

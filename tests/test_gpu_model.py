@@ -115,8 +115,10 @@ def test_block_tables_match_separate_launches(dim, heads, win):
         m.zero_grad(set_to_none=True)
         if fused:
             r = m.block_tables()
+            assert isinstance(r, sw.ProjFoldTables)
         else:
             r = m.gemm_biases() + m.cpb_tables()
+            assert not isinstance(r, sw.ProjFoldTables)
         torch.manual_seed(1)
         g = [None] + [torch.randn_like(t) for t in r[1:]]
         torch.autograd.backward([t for t in r[1:]], g[1:])
@@ -130,7 +132,30 @@ def test_block_tables_match_separate_launches(dim, heads, win):
     assert "proj.weight" not in ga and set(ga) | {"proj.weight"} == set(gb) and len(ga) >= 6, sorted(ga)
     for n in ga:
         assert torch.allclose(ga[n], gb[n], rtol=1e-4, atol=1e-5), n  # d v_bias: f32 atomics
-    assert m._proj_fold
+
+
+def test_forward_tokens_proj_grad_same_for_either_bias_source():
+    """forward_tokens keys the proj Linear's v_bias weight-gradient share on the biases it is
+    given (ProjFoldTables from the fused tables: W_proj detached there), not on state a previous
+    block_tables() call left behind: passing gemm_biases() (W_proj NOT detached) after a fused
+    call must not double d proj.weight."""
+    import hvamd.swinv2 as sw
+    torch.manual_seed(2)
+    m = sw.WindowAttention(96, (7, 7), 3).cuda()
+    m.input_resolution, m.shift_size = (14, 14), 0
+    with torch.no_grad():
+        m.v_bias.normal_()
+    x = torch.randn(2, 196, 96, device="cuda").bfloat16()
+    grads = []
+    for mode in ("fused", "gemm_biases"):
+        m.zero_grad(set_to_none=True)
+        _ = m.block_tables()  # leaves whatever state a fused call leaves
+        biases = m.block_tables() if mode == "fused" else m.gemm_biases() + m.cpb_tables()
+        y = m.forward_tokens(x, 14, 14, 0, biases=biases)
+        y.float().square().mean().backward()
+        grads.append(m.proj.weight.grad.clone())
+    rel = ((grads[0] - grads[1]).norm() / grads[1].norm()).item()
+    assert rel < 1e-2, rel
 
 
 @pytest.mark.parametrize("dim,T", [(96, 6272), (384, 1568), (768, 2048)])

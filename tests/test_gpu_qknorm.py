@@ -240,7 +240,7 @@ def test_block_qk_epilogue_matches_raw(monkeypatch):
     x = torch.randn(4, 28 * 28, 96, device="cuda")
     res = []
     for on in (False, True):
-        monkeypatch.setattr(sw, "_QK_EPILOGUE", on)
+        monkeypatch.setattr(sw.OPTIONS, "qk_epilogue", on)
         blk.zero_grad(set_to_none=True)
         y = blk(x)
         loss = y.float().square().mean()

@@ -277,7 +277,7 @@ def test_wmsa_large_backward_paths_agree(monkeypatch, B, H, W, nh, win, shift, s
     gout = torch.from_numpy(np.random.default_rng(6).standard_normal((B, H * W, 32 * nh)).astype(np.float32))
     res = {}
     for keep in (True, False):
-        monkeypatch.setattr(ops, "_WMSA_LARGE_LSE", keep)
+        monkeypatch.setattr(ops.OPTIONS, "wmsa_large_lse", keep)
         q = qkv.cuda().bfloat16().requires_grad_(True)
         t = tab.cuda().requires_grad_(True)
         s = scale.cuda().requires_grad_(True)

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
         exported = {ln.split()[-1] for ln in nm.stdout.splitlines() if " T hvk_" in ln}
         assert exported == set(declared), exported ^ set(declared)
     lib = _lib.load()
-    assert lib.hvk_abi_version() == 9
+    assert lib.hvk_abi_version() == _lib.ABI_VERSION
     # [accumulators][dscale nH][dq_bias 32 nH] floats
     assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
     assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4
@@ -40,6 +40,53 @@ def test_library_exports_every_declared_symbol():
     assert lib.hvk_weight_grad_workspace(802816, 288, 96) == 256 * (288 * 96 + 288) * 4
     assert lib.hvk_weight_grad_supported(802816 + 16, 288, 96) == 0  # M % 32
     assert lib.hvk_weight_grad_supported(4096, 100, 96) == 0
+
+
+def test_abi_version_agrees_everywhere():
+    """include/hvk.h's HVK_ABI_VERSION, the library's hvk_abi_version(), the Python binding's
+    ABI_VERSION and the version INTEGRATION.md's binding example asserts are one number."""
+    from hvamd import _lib
+    hdr = open(os.path.join(ROOT, "include", "hvk.h")).read()
+    m = re.search(r"#define\s+HVK_ABI_VERSION\s+(\d+)", hdr)
+    assert m, "include/hvk.h defines no HVK_ABI_VERSION"
+    v = int(m.group(1))
+    assert _lib.ABI_VERSION == v
+    assert _lib.load().hvk_abi_version() == v
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    asserted = [int(x) for x in re.findall(r"hvk_abi_version\(\)\s*==\s*(\d+)", doc)]
+    assert asserted and all(a == v for a in asserted), (asserted, v)
+
+
+def test_product_modules_read_no_environment():
+    """Routing switches live in hvamd.options (printed by bench.py), not in the environment:
+    no product module reads os.environ / os.getenv except _lib.py's HVK_LIB_PATH."""
+    pkg = os.path.join(ROOT, "hierarchical-vision_amd")
+    for fn in sorted(os.listdir(pkg)):
+        if not fn.endswith(".py"):
+            continue
+        for ln in open(os.path.join(pkg, fn)):
+            if "os.environ" in ln or "getenv(" in ln:
+                assert fn == "_lib.py" and "HVK_LIB_PATH" in ln, (fn, ln)
+
+
+def test_bounds_build_not_broken():
+    """__graft_entry__.build() keeps the bounds-checking debug build optional for the product,
+    but records its failure; W-MSA memory-safety coverage (tests/test_gpu_wmsa.py) must not
+    disappear silently."""
+    marker = os.path.join(ROOT, "hierarchical-vision_amd", "BOUNDS_BUILD_FAILED.txt")
+    assert not os.path.exists(marker), open(marker).read()
+
+
+def test_host_options_object():
+    from hvamd import options
+    assert options.non_default() == {}
+    with options.override(qk_epilogue=False, mlp_fused=0):
+        assert options.OPTIONS.qk_epilogue is False and options.OPTIONS.mlp_fused is False
+        assert set(options.non_default()) == {"qk_epilogue", "mlp_fused"}
+    assert options.non_default() == {}
+    assert options.parse("head_gemm=false") == {"head_gemm": 0}
+    with pytest.raises(KeyError):
+        options.set(no_such_option=1)
 
 
 def test_library_rejects_bad_arguments_without_gpu():

@@ -1,7 +1,7 @@
 # PMC passes for the W-MSA kernels at the SwinV2-T stage-0 shape (separate rocprofv3 runs,
 # counters only with the kernel trace, per MI355X_MICROARCH.md "rocprofv3 PMC slots").
 #   bash tools/pmc_wmsa.sh [fwd|bwd] [tag] [passes: sq,fetch,write,lds]
-# Environment (e.g. HVK_WMSA_FWD_V1=1) is inherited by the profiled process.
+# Environment is inherited by the profiled process.
 set -o pipefail
 ONLY=${1:-fwd}
 TAG=${2:-$ONLY}
