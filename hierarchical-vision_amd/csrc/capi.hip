@@ -39,6 +39,7 @@ OptDef g_opts[HVK_OPT_COUNT] = {
     {"tile_wide", -1, -1, 1},
     {"dw_tile", 5, 4, 8},
     {"gemm_xr", 0, 0, 2},
+    {"gemm_wide", 0, 0, 1},
 };
 int find_opt(const char* name) {
   if (!name) return -1;

@@ -1,6 +1,7 @@
 // Persistent row-range GEMM (gemm_xr.hip): host entry used by the tiled-GEMM launchers.
 #pragma once
 #include <hip/hip_runtime.h>
+// (also declares hvk_wide below)
 
 typedef unsigned short hvk_bf16;
 
@@ -20,3 +21,11 @@ int launch(int epi, const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk
            int N, int K, hipStream_t st);
 bool plan(int M, int N, int K, Args& a, int& mg);
 }  // namespace hvk_xr
+
+// Whole-row 208 x 384 tile GEMM (gemm_wide.hip): epi 0 / 1 / 4 as the tiled kernels; returns -1
+// (nothing launched) where it is not built, else an HVK status.
+namespace hvk_wide {
+bool supported(int M, int N, int K);
+int launch(int epi, const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2, int M,
+           int N, int K, hipStream_t st, float* rn, const float* qscale);
+}  // namespace hvk_wide

@@ -33,6 +33,7 @@ enum HvkOption {
   HVK_OPT_TILE_WIDE,            // tiled GEMM: -1 by shape, 0 128-column, 1 192-column tiles
   HVK_OPT_DW_TILE,              // weight gradient, 192-multiple shapes: tile variant 4..8
   HVK_OPT_GEMM_XR,              // tiled GEMM: persistent row-range kernel where it fits (1, 2: DMA interleaved), 0 off
+  HVK_OPT_GEMM_WIDE,            // tiled GEMM: 1 the 208 x 384 whole-row tile where built (gemm_wide.hip), 0 off
   HVK_OPT_COUNT
 };
 long long hvk_opt(int id);
