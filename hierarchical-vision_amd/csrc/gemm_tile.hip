@@ -691,7 +691,7 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   // input gradient, K = 1152: profiles/round4/tile_width_staged/); option "tile_wide" 0 / 1
   // forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
-  if (EPI != 2 && hvk_opt(HVK_OPT_GEMM_WIDE)) {  // the 208 x 384 whole-row tile where built
+  if (hvk_opt(HVK_OPT_GEMM_WIDE)) {  // the 208 x 384 whole-row tile where built
     const int r = hvk_wide::launch(EPI, X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     if (r >= 0) return r;
   }

@@ -1,7 +1,8 @@
 // Whole-row MFMA GEMM for the stage-2 SwinV2 Linears (M = 50 176 tokens at bs256):
 //   Y[M, N] = X[M, K] W[N, K]^T (+ bias)  -- F.linear of swinv2.py:58-62, 220, 262, 492 and the
-//   input gradients (W = weight^T), forward epilogues EPI 0 (plain), 1 (fc1: h and GELU(h)),
-//   4 (qkv: q / k head slices L2-normalised, q times the logit scale, swinv2.py:229-231).
+//   input gradients (W = weight^T), epilogues EPI 0 (plain), 1 (fc1: h and GELU(h)), 2 (fc2's
+//   input gradient through the activation: gh = (gy W) * GELU'(h), h read from Y2), 4 (qkv: q / k
+//   head slices L2-normalised, q times the logit scale, swinv2.py:229-231).
 //
 // Why another tile: the 128-row tiles (gemm_tile.hip) run two workgroups per CU and stream
 // (128 + 192) x 64 x 2 B from L2 per 1.57 M MACs, 0.026 B/MAC, while a CU's L2->LDS DMA path
@@ -220,14 +221,35 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_wide_kernel(const hvk_bf16* _
       bv[4 * q] = b.x; bv[4 * q + 1] = b.y; bv[4 * q + 2] = b.z; bv[4 * q + 3] = b.w;
     }
   }
+  // EPI 2: the saved pre-activation h of this lane's 12 columns, two row tiles ahead
+  constexpr int HD = 2;
+  uint2 hq[EPI == 2 ? HD + 1 : 1][3];
+  auto load_h = [&](int a) {
+    if constexpr (EPI == 2) {
+      int row = m0 + 16 * a + li;
+      if (row >= M) row = M - 1;  // never stored
+      const uint2* hp = reinterpret_cast<const uint2*>(Y2 + (size_t)row * N + n0 + c0);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) hq[a % (HD + 1)][q] = hp[q];
+    }
+  };
+#pragma unroll
+  for (int a = 0; a < HD; ++a) load_h(a);
 #pragma unroll
   for (int a = 0; a < WMT; ++a) {
     const int r = 16 * a + li;
+    if (a + HD < WMT) load_h(a + HD);
 #pragma unroll
     for (int t = 0; t < TW; ++t) {
       // columns c0 + 4t .. + 3 = acc rows 4g .. 4g + 3 of column tile t (wperm)
-      const float v0 = acc[a][t][0] + bv[4 * t], v1 = acc[a][t][1] + bv[4 * t + 1];
-      const float v2 = acc[a][t][2] + bv[4 * t + 2], v3 = acc[a][t][3] + bv[4 * t + 3];
+      float v0 = acc[a][t][0] + bv[4 * t], v1 = acc[a][t][1] + bv[4 * t + 1];
+      float v2 = acc[a][t][2] + bv[4 * t + 2], v3 = acc[a][t][3] + bv[4 * t + 3];
+      if constexpr (EPI == 2) {  // gh = (gy W) * GELU'(h) (the fc2 input gradient, swinv2.py:60-61)
+        const uint2 h2 = hq[a % (HD + 1)][t];
+        const hvk_gelu::f32x2 d0 = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hvk_lo(h2.x), hvk_hi(h2.x)});
+        const hvk_gelu::f32x2 d1 = hvk_gelu::gelu_grad2(hvk_gelu::f32x2{hvk_lo(h2.y), hvk_hi(h2.y)});
+        v0 *= d0.x; v1 *= d0.y; v2 *= d1.x; v3 *= d1.y;
+      }
       const uint2 pk = make_uint2(hvk_pack2(v0, v1), hvk_pack2(v2, v3));
       *reinterpret_cast<uint2*>(smem + img_off(r, 2 * (c0 + 4 * t))) = pk;
     }
@@ -299,7 +321,7 @@ int launch_wide_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   }
   const int mtiles = (M + WBM - 1) / WBM;
   const dim3 grid((mtiles + 7) / 8 * 8 * (N / WBN));
-  const double bytes = 2.0 * ((double)M * K + (double)N * K + (double)M * N) + (EPI == 1 ? 2.0 * M * N : 0.0) +
+  const double bytes = 2.0 * ((double)M * K + (double)N * K + (double)M * N) + (EPI == 1 || EPI == 2 ? 2.0 * M * N : 0.0) +
                        (EPI == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0);
   hvk_timer_shape("gemm_wide", EPI, WBM, M, N, K, bytes);
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_wide_kernel<EPI>), grid, dim3(THREADS), LDS, st, X, W,
@@ -323,6 +345,7 @@ int launch(int epi, const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk
   switch (epi) {
     case 0: return launch_wide_<0>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     case 1: return launch_wide_<1>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
+    case 2: return launch_wide_<2>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     case 4: return launch_wide_<4>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     default: return -1;
   }

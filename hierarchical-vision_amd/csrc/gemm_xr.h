@@ -22,7 +22,7 @@ int launch(int epi, const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk
 bool plan(int M, int N, int K, Args& a, int& mg);
 }  // namespace hvk_xr
 
-// Whole-row 208 x 384 tile GEMM (gemm_wide.hip): epi 0 / 1 / 4 as the tiled kernels; returns -1
+// Whole-row 208 x 384 tile GEMM (gemm_wide.hip): epi 0 / 1 / 2 / 4 as the tiled kernels; returns -1
 // (nothing launched) where it is not built, else an HVK status.
 namespace hvk_wide {
 bool supported(int M, int N, int K);

@@ -224,9 +224,9 @@ class MultitaskHead(torch.nn.Module):
         self.heads = torch.nn.ModuleList([torch.nn.Linear(num_features, n) for n in self.num_classes])
 
     def forward(self, x):
-        from . import ops, swinv2
+        from .options import OPTIONS
         ws = [h.weight for h in self.heads]
-        if swinv2._HEAD_GEMM and torch.is_autocast_enabled() and ops.head_supported(x, ws):
+        if OPTIONS.head_gemm and torch.is_autocast_enabled() and ops.head_supported(x, ws):
             # all tiers as one GEMM over the concatenated classes (libhvk head kernels)
             return list(ops.head_linear(x, ws, [h.bias for h in self.heads]))
         return [head(x) for head in self.heads]

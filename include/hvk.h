@@ -48,7 +48,7 @@ const char* hvk_last_error_string(void);
  *   dw_tile               weight gradient at 192-multiple shapes: tile variant 4..8 (default 5)
  *   gemm_xr               tiled GEMM: 0 (default) tile kernel, 1 / 2 the persistent row-range
  *                         kernel (gemm_xr.hip; bit-identical, measured slower)
- *   gemm_wide             tiled GEMM forward epilogues 0 / 1 / 4: 1 the 208 x 384 whole-row tile,
+ *   gemm_wide             tiled GEMM (epilogues 0 / 1 / 2 / 4): 1 the 208 x 384 whole-row tile,
  *                         one 512-thread workgroup per CU (gemm_wide.hip; bit-identical) where
  *                         built (N % 384, K % 32, M >= 1664), 0 the 128-row tiles */
 int hvk_set_option(const char* name, long long value, long long* previous);

@@ -66,6 +66,27 @@ def test_wide_gelu_bit_identical(M, K, N):
     assert rel < 1e-2, rel
 
 
+@pytest.mark.parametrize("M,K,N", [(50176, 384, 1536), (50171, 384, 1536), (12544, 768, 3072)])
+def test_wide_gelu_bwd_bit_identical(M, K, N):
+    """fc2's input gradient through GELU' (EPI 2, hvk_gemm_gelu_bwd): gh = bf16((gy W) GELU'(h))
+    with h read in the accumulator layout, bit-identical to the 128-row kernel."""
+    from hvamd import _lib
+    gy, w, _ = _case(M, K, N, M + 5 * N, bias=False)
+    h = torch.randn(M, N, device="cuda").bfloat16()
+    out = []
+    for mode in (0, 1):
+        gh = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        _run("hvk_gemm_gelu_bwd", mode, _lib.ptr(gy), _lib.ptr(w), _lib.ptr(h), _lib.ptr(gh), M, K, N, _lib.stream())
+        out.append(gh)
+    assert torch.isnan(out[1][M:].float()).all()
+    assert torch.equal(_bits(out[0][:M]), _bits(out[1][:M]))
+    hf = h.float()
+    dg = 0.5 * (1 + torch.erf(hf / 2 ** 0.5)) + hf * torch.exp(-0.5 * hf * hf) / (2 * torch.pi) ** 0.5
+    ref = (gy.float() @ w.float().t()) * dg
+    rel = ((out[1][:M].float() - ref).norm() / ref.norm()).item()
+    assert rel < 1e-2, rel
+
+
 @pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (49999, 384, 1152), (50176, 512, 1536)])
 def test_wide_qkv_epilogue_bit_identical(M, K, N):
     """The qkv epilogue (EPI 4): q / k head slices normalised on the rounded values (the head's

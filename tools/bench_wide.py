@@ -12,8 +12,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# name, M, K, N, epilogue (0 plain, 1 fc1 + GELU, 4 qkv)
+# name, M, K, N, epilogue (0 plain, 1 fc1 + GELU, 2 fc2 input grad through GELU', 4 qkv)
 SHAPES = [("s2.qkv", 50176, 384, 1152, 4), ("s2.proj", 50176, 384, 384, 0), ("s2.fc1", 50176, 384, 1536, 1),
+          ("s2.fc2.dx", 50176, 384, 1536, 2),
           ("s2.fc2", 50176, 1536, 384, 0), ("s2.proj.dx", 50176, 384, 384, 0), ("s2.qkv.dx", 50176, 1152, 384, 0),
           ("s2.fc1.dx", 50176, 1536, 384, 0), ("s1.merge", 50176, 768, 384, 0), ("s1.merge.dx", 50176, 384, 768, 0),
           ("s3.fc2", 12544, 3072, 768, 0), ("s3.qkv", 12544, 768, 2304, 4)]
@@ -44,6 +45,9 @@ def main():
             if epi == 4:
                 _lib.call("hvk_gemm_qkv_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(rn),
                           _lib.ptr(sc), M, K, N, _lib.stream())
+            elif epi == 2:
+                _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(y2), _lib.ptr(y), M, K, N,
+                          _lib.stream())
             elif epi == 1:
                 _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2), M, K,
                           N, _lib.stream())
@@ -64,7 +68,7 @@ def main():
                     torch.cuda.synchronize()
                     times[mode].append(1000 * s.elapsed_time(e) / a.iters)
         t0, t1 = statistics.median(times[0]), statistics.median(times[1])
-        byt = 2.0 * (M * K + N * K + M * N) + (2.0 * M * N if epi == 1 else 0) + (8.0 * M * N / 96 if epi == 4 else 0)
+        byt = 2.0 * (M * K + N * K + M * N) + (2.0 * M * N if epi in (1, 2) else 0) + (8.0 * M * N / 96 if epi == 4 else 0)
         roof = max(2.0 * M * N * K / 2.5e15, byt / 8e12) * 1e6
         tot[0] += t0
         tot[1] += t1
