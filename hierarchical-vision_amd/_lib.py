@@ -74,6 +74,11 @@ SIGNATURES = {
     "hvk_linear_gelu_bwd_supported": (_i, [_i, _i, _i]),
     "hvk_mlp_fwd_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
+    "hvk_linear_ln_supported": (_i, [_i, _i, _i]),
+    "hvk_linear_ln_fwd": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p, _p, _p, _p]),
+    "hvk_mlp_ln_supported": (_i, [_i, _i, _i, _i]),
+    "hvk_mlp_ln_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p, _p,
+                            _p]),
     "hvk_mlp_bwd_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_bwd": (_i, [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
     "hvk_linear_gelu_in_supported": (_i, [_i, _i, _i]),
@@ -105,7 +110,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 10  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
+ABI_VERSION = 11  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
 
 
 def load():

@@ -23,6 +23,10 @@
 
 namespace {
 
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 template <int K, int BN>
 struct GCfg {
   static_assert(K % 16 == 0 && BN % 32 == 0, "K multiple of 16, BN multiple of 32");
@@ -49,6 +53,135 @@ __device__ __forceinline__ int perm_row(int p) {
 // (row li + 8, j), lanes li >= 8 (row li - 8, j+1) and (row li, j+1) -- two stores of 8 rows x
 // 128 B each, every line written whole by one instruction.
 
+// ---- post-norm LayerNorm + residual epilogue (EPI 5 of linear_kernel, mlp_fwd_kernel<LN>) --------
+// The res-post-norm `x = x0 + drop_path(norm(a))` of swinv2.py:431 / 434 (and the plain norm of
+// PatchEmbed, 656, with no x0) applied to the GEMM's bf16 output a where ONE workgroup holds whole
+// C = 96 rows (stage 0): a is still stored (the LayerNorm backward reads it), but the separate
+// LayerNorm launch -- its re-read of a and its own pass over the rows -- disappears.  Per 16-row
+// tile a wave hands its rows through a 768-B LDS staging buffer, four rows at a time, into
+// ln_fwd_kernel<8, 16>'s lane layout (layernorm.hip: 16 lanes per row, channel groups of 4 at
+// 4 (16 i + t)) and runs that kernel's arithmetic on it, so x, xb, mean and rstd are bit-identical
+// to the two-launch path (tests/test_gpu_linear_ln.py).
+struct LnEpi {
+  const float* abias;   // [96] the Linear's bias, added in f32 inside the norm (or null)
+  const float* x0;      // [M, 96] f32 residual stream (null: plain norm)
+  const float* gamma;   // [96]
+  const float* beta;    // [96]
+  const float* sscale;  // [M / rows_per_sample] DropPath factor per sample (or null)
+  int rows_per_sample;
+  float eps;
+  float* x;             // [M, 96] f32 out
+  hvk_bf16* xb;         // [M, 96] bf16 copy (next GEMM operand) or null
+  float* mean;          // [M]
+  float* rstd;          // [M]
+};
+namespace ln96 {
+constexpr int C = 96, TPR = 16, NG = 2, EPT = 8, STAGE_BYTES = 4 * C * 2;
+constexpr int PARAM_BYTES = 3 * C * 4;
+// gamma, beta, abias as a [3][96] f32 table in LDS (one copy per workgroup, written before the
+// workgroup's first barrier), read per pass instead of pinning 24 VGPRs per lane
+struct Params {
+  uint32_t lds;  // LDS byte address of the table
+};
+__device__ __forceinline__ bool grp_ok(int t, int i) { return 4 * (i * TPR + t) < C; }
+__device__ __forceinline__ void load_params(const LnEpi& p, float* tab) {
+  for (int e = threadIdx.x; e < 3 * C; e += blockDim.x) {
+    const int k = e / C, c = e - k * C;
+    tab[e] = k == 0 ? p.gamma[c] : (k == 1 ? p.beta[c] : (p.abias ? p.abias[c] : 0.f));
+  }
+}
+__device__ __forceinline__ float4 param4(const Params& q, int k, int c) {
+  const hvk_f32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) hvk_f32x4*>(
+      (const __attribute__((address_space(3))) char*)(size_t)(q.lds + (k * C + c) * 4));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+// the residual rows of a 16-row tile in the norm's layout (pass pp: rows 4 pp + lane / 16), one
+// tile ahead of their use; rows past M and absent x0 read 0 (buffer view, no branch)
+__device__ __forceinline__ void load_x0(const LnEpi& p, int row0, int M, uint4 (&x0v)[4][NG]) {
+  const int t = threadIdx.x & (TPR - 1), sub = (threadIdx.x & 63) / TPR;
+  const auto r = hvk_tile_rsrc(p.x0, row0, p.x0 ? M : 0, C * 4);
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int c = 4 * (i * TPR + t);
+      x0v[pp][i] = hvk_bld16(r, grp_ok(t, i) ? (uint32_t)((4 * pp + sub) * C + c) * 4 : HVK_OOB);
+    }
+}
+// av[j]: this lane's packed a of row li, columns 32 j + 8 g .. +7 (the skinny kernels' layout)
+__device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t stage, const uint4 (&av)[3],
+                                     const uint4 (&x0v)[4][NG], int row0, int M) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  const int t = lane & (TPR - 1), sub = lane / TPR;
+  const float invC = 1.f / C;
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    if ((li >> 2) == pp) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        *reinterpret_cast<__attribute__((address_space(3))) hvk_u32x4*>((__attribute__((address_space(3))) char*)(size_t)(stage + (li & 3) * C * 2 + (32 * j + 8 * g) * 2)) =
+            __builtin_bit_cast(hvk_u32x4, av[j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int row = row0 + 4 * pp + sub;
+    float v[EPT];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      if (grp_ok(t, i)) {
+        const int c = 4 * (i * TPR + t);
+        const hvk_u32x2 u = *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x2*>(
+            (const __attribute__((address_space(3))) char*)(size_t)(stage + sub * C * 2 + c * 2));
+        v[4 * i] = hvk_lo(u[0]); v[4 * i + 1] = hvk_hi(u[0]); v[4 * i + 2] = hvk_lo(u[1]); v[4 * i + 3] = hvk_hi(u[1]);
+        const float4 ab = param4(q, 2, c);
+        const float abv[4] = {ab.x, ab.y, ab.z, ab.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[4 * i + j] += abv[j]; s += v[4 * i + j]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staging reads are back before the next pass's writes
+#pragma unroll
+    for (int m = TPR / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    const float mu = s * invC;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NG; ++i)
+      if (grp_ok(t, i)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { const float d = v[4 * i + j] - mu; ss += d * d; }
+      }
+#pragma unroll
+    for (int m = TPR / 2; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+    const float rs = rsqrtf(ss * invC + p.eps);
+    if (row >= M) continue;
+    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
+    const size_t rb = (size_t)row * C;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      if (!grp_ok(t, i)) continue;
+      const int c = 4 * (i * TPR + t);
+      float r[4] = {__uint_as_float(x0v[pp][i].x), __uint_as_float(x0v[pp][i].y), __uint_as_float(x0v[pp][i].z),
+                    __uint_as_float(x0v[pp][i].w)};
+      const float4 g4 = param4(q, 0, c), b4 = param4(q, 1, c);
+      const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] += ((v[4 * i + j] - mu) * rs * gm[j] + bt[j]) * sc;
+      const uint4 xr = make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3]));
+      if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
+      else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
+      if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(r[0], r[1]), hvk_pack2(r[2], r[3]));
+    }
+    if (t == 0) {
+      p.mean[row] = mu;
+      p.rstd[row] = rs;
+    }
+  }
+}
+}  // namespace ln96
+
 // EPI 0: Y = acc (+ bias).  EPI 1 (fc1): Y = h = bf16(acc + bias) and Y2 = GELU(h), the
 // bf16 pre-activation kept for the backward and the activation for fc2 (the reference's
 // F.linear(+bias) -> nn.GELU on the bf16 tensor, swinv2.py:58-62).
@@ -61,6 +194,8 @@ __device__ __forceinline__ int perm_row(int p) {
 // EPI 4 (the qkv Linear of a w <= 8 W-MSA block): EPI 0 with every q and k head slice (columns
 // < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
 // 1 / max(||x||, eps) stored to rn [M, 2N/96] (passed in csum).
+// EPI 5 (C = 96, one column block): Y = a = bf16(acc) and the post-norm LayerNorm + residual of
+// a (LnEpi, above) in the same pass.
 template <int K, int BN, int WAVES, bool PREF, bool BIAS, int EPI = 0>
 __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __restrict__ X,
                                                           const hvk_bf16* __restrict__ W,
@@ -69,8 +204,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
                                                           hvk_bf16* __restrict__ Y2, int M, int N,
                                                           int ncb, int row_groups,
                                                           float* __restrict__ csum = nullptr,
-                                                          const float* __restrict__ qscale = nullptr) {
+                                                          const float* __restrict__ qscale = nullptr,
+                                                          LnEpi ln = LnEpi{}) {
   using G = GCfg<K, BN>;
+  static_assert(EPI != 5 || BN == 96, "the LayerNorm epilogue holds whole C = 96 rows");
   constexpr int kThreads = 64 * WAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint4* wl = reinterpret_cast<uint4*>(smem);                                // [NT][U4][16]
@@ -92,6 +229,8 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
   }
   if (BIAS)
     for (int e = threadIdx.x; e < BN; e += kThreads) bl[e] = bias[n0 + e];
+  if constexpr (EPI == 5)
+    ln96::load_params(ln, reinterpret_cast<float*>(smem + G::LDS + WAVES * ln96::STAGE_BYTES));
   __syncthreads();
 
   // wave-uniform tile index: every global access goes through a buffer view of its 16-row
@@ -126,6 +265,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
   load_x(tile, xf);
   uint4 hf[EPI == 2 ? G::NT / 2 : 1];
   load_h(tile, hf);
+  // EPI 5: the norm's parameters (its lane layout), and the residual rows one tile ahead like X
+  const uint32_t lstage = lds_addr(smem) + (uint32_t)G::LDS + (uint32_t)wave * ln96::STAGE_BYTES;
+  const ln96::Params lnq{lds_addr(smem) + (uint32_t)G::LDS + (uint32_t)WAVES * ln96::STAGE_BYTES};
   // the first tile's operands land before the loop (the loop header's wait then serves only
   // the back edge, counted, instead of vmcnt(0) on every iteration)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -148,6 +290,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
     if (PREF) load_x(tile + stride, xn);
     uint4 hn[EPI == 2 ? G::NT / 2 : 1];
     load_h(tile + stride, hn);
+    // EPI 5: this tile's residual rows (issued here, used by the norm after the MFMAs and the a
+    // stores; a tile ahead they held 32 more VGPRs: 164, 3 waves per SIMD)
+    uint4 x0f[EPI == 5 ? 4 : 1][ln96::NG];
+    if constexpr (EPI == 5) ln96::load_x0(ln, 16 * tile, M, x0f);
     __builtin_amdgcn_sched_barrier(0);  // the next tile's loads issue here, not after the MFMAs
     hvk_f32x4 acc[G::NT];
 #pragma unroll
@@ -197,6 +343,7 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           hvk_bst16(ry2, o + 16 * N, b0);
         }
       };
+      uint4 av[EPI == 5 ? G::NT / 2 : 1];   // EPI 5: the row's packed a, for the norm
       float rq[EPI == 4 ? G::NT / 2 : 1];  // EPI 4: the row's 1/||x|| per head slice
 #pragma unroll
       for (int j = 0; j < (EPI == 4 ? G::NT / 2 : 1); ++j) rq[j] = 0.f;
@@ -254,8 +401,10 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
           }
           gl = hvk_pack8(u);
         }
+        if constexpr (EPI == 5) av[j] = hv;
         put(j, hv, gl, EPI == 1 && (HVK_NT_SAVED & 1));
       }
+      if constexpr (EPI == 5) ln96::tile(ln, lnq, lstage, av, x0f, 16 * tile, M);
       if constexpr (EPI == 4) {
         // the row's 1/||x|| per q / k head slice j (all 4 lanes of a row hold every one): lane g
         // stores slices g, g + 4, ..., a buffer store dropped past M and past the q / k columns
@@ -306,7 +455,9 @@ __global__ __launch_bounds__(64 * WAVES) void linear_kernel(const hvk_bf16* __re
 // so the chain needs no data movement and fc2 accumulates its 12 chunks in the same order as
 // linear_kernel<384, 96> (bit-identical y).  Saves fc2's re-read of GELU(h) (616 MB per block
 // at bs256).
-template <int WAVES>
+// LN: the block's post-norm LayerNorm + residual of y in the same pass (ln96, above; y = a is
+// still stored for the LayerNorm backward).
+template <int WAVES, bool LN = false>
 __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __restrict__ X,
                                                            const hvk_bf16* __restrict__ W1,
                                                            const float* __restrict__ b1,
@@ -315,7 +466,7 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
                                                            hvk_bf16* __restrict__ H,
                                                            hvk_bf16* __restrict__ Gh,
                                                            hvk_bf16* __restrict__ Y, int M,
-                                                           int row_groups) {
+                                                           int row_groups, LnEpi ln = LnEpi{}) {
   using G1 = GCfg<96, 384>;   // fc1: K 96, 384 outputs
   using G2 = GCfg<384, 96>;   // fc2: K 384, 96 outputs
   constexpr int K = 96, N1 = 384, N2 = 96, kThreads = 64 * WAVES;
@@ -336,6 +487,7 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
   }
   for (int e = threadIdx.x; e < N1; e += kThreads) b1l[e] = b1[e];
   for (int e = threadIdx.x; e < N2; e += kThreads) b2l[e] = b2 ? b2[e] : 0.f;
+  if constexpr (LN) ln96::load_params(ln, b2l + N2 + WAVES * ln96::STAGE_BYTES / 4);
   __syncthreads();
 
   // branch-free global accesses through 16-row tile buffer views (see linear_kernel)
@@ -351,6 +503,10 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
   };
   uint4 xf[G1::KS];
   load_x(tile, xf);
+  const uint32_t lstage = lds_addr(smem) + (uint32_t)(b2l + N2 - reinterpret_cast<float*>(smem)) * 4 +
+                          (uint32_t)wave * ln96::STAGE_BYTES;
+  const ln96::Params lnq{lds_addr(smem) + (uint32_t)(b2l + N2 - reinterpret_cast<float*>(smem)) * 4 +
+                         (uint32_t)WAVES * ln96::STAGE_BYTES};
   // the first tile's operands land before the loop: otherwise the loop header's wait serves
   // both entries and becomes vmcnt(0) on every iteration (draining the stores in flight)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -360,6 +516,10 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
     asm volatile("" ::: "memory");
     uint4 xn[G1::KS];
     load_x(tile + stride, xn);
+    // LN: this tile's residual rows, issued here: they land under the tile's 144 MFMAs (a tile
+    // ahead they would hold 32 more VGPRs in a kernel at the 256 limit)
+    uint4 x0f[LN ? 4 : 1][ln96::NG];
+    if constexpr (LN) ln96::load_x0(ln, 16 * tile, M, x0f);
     __builtin_amdgcn_sched_barrier(0);  // the next tile's loads issue here, not after the MFMAs
     const auto rh = hvk_tile_rsrc(H, 16 * tile, M, N1 * 2), rg2 = hvk_tile_rsrc(Gh, 16 * tile, M, N1 * 2);
     const auto ry = hvk_tile_rsrc(Y, 16 * tile, M, N2 * 2);
@@ -416,6 +576,7 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
 #pragma unroll
       for (int t = 0; t < G2::NT; ++t) acc2[t] = hvk_mfma16(w2l[(t * G2::U4 + 4 * j + g) * 16 + li], gv, acc2[t]);
     }
+    uint4 av[3];  // LN: the row's packed y
 #pragma unroll
     for (int j = 0; j < G2::NT / 2; ++j) {
       float v[8];
@@ -427,6 +588,7 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += b2l[32 * j + 8 * g + e];  // 0 without a bias
       const uint4 yv = hvk_pack8(v);
+      av[j] = yv;
       if (!HVK_LIN_PAIRSTORE || j == G2::NT / 2 - 1) {  // the third slice stores alone
         hvk_bst16(ry, yo + 64 * j, yv);
       } else if (j % 2 == 0) {
@@ -438,6 +600,7 @@ __global__ __launch_bounds__(64 * WAVES) void mlp_fwd_kernel(const hvk_bf16* __r
         hvk_bst16(ry, yp + 64 * (j - 1) + 16 * N2, b0);
       }
     }
+    if constexpr (LN) ln96::tile(ln, lnq, lstage, av, x0f, 16 * tile, M);
 #pragma unroll
     for (int s = 0; s < G1::KS; ++s) xf[s] = xn[s];
   }
@@ -590,8 +753,11 @@ int g_cu_count = 0;
 template <int K, int BN, int WAVES, bool PREF, int EPI = 0>
 int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, int M,
                   int N, hipStream_t st, hvk_bf16* Y2 = nullptr, float* csum = nullptr,
-                  const float* qscale = nullptr) {
-  using G = GCfg<K, BN>;
+                  const float* qscale = nullptr, const LnEpi& ln = LnEpi{}) {
+  using G0 = GCfg<K, BN>;
+  struct G {  // EPI 5: + one 768-B norm staging buffer per wave
+    enum : size_t { LDS = G0::LDS + (EPI == 5 ? (size_t)WAVES * ln96::STAGE_BYTES + ln96::PARAM_BYTES : 0) };
+  };
   constexpr int kThreads = 64 * WAVES;
   auto kb = &linear_kernel<K, BN, WAVES, PREF, true, EPI>;
   auto kn = &linear_kernel<K, BN, WAVES, PREF, false, EPI>;
@@ -627,13 +793,14 @@ int launch_linear(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_b
   // EPI 4 writes 1/||.|| per token and q / k head (f32)
   hvk_timer_shape("linear", EPI, BN, M, N, K,
                   2.0 * ((double)M * K + (double)N * K + (double)M * N) +
-                      (EPI == 1 || EPI == 2 ? 2.0 * M * N : 0.0) + (EPI == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0));
+                      (EPI == 1 || EPI == 2 ? 2.0 * M * N : 0.0) + (EPI == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0) +
+                      (EPI == 5 ? (ln.x0 ? 4.0 : 0.0) * M * N + (ln.xb ? 6.0 : 4.0) * M * N + 8.0 * M : 0.0));
   if (bias)
     HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kb, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
-                       ncb, row_groups, csum, qscale);
+                       ncb, row_groups, csum, qscale, ln);
   else
     HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, flops, kn, grid, dim3(kThreads), G::LDS, st, X, W, bias, Y, Y2, M, N,
-                       ncb, row_groups, csum, qscale);
+                       ncb, row_groups, csum, qscale, ln);
   HVK_CHECK_LAUNCH("hvk_linear");
   return HVK_OK;
 }
@@ -770,13 +937,13 @@ int hvk_mlp_fwd_supported(int M, int K, int N1, int N2) {
          mlp_lds_granted(reinterpret_cast<const void*>(&mlp_fwd_kernel<8>), kMlpFwdLds, g_mlp_fwd_lds);
 }
 
-int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
-                void* g, void* y, int M, int K, int N1, int N2, void* stream) {
-  if (!x || !w1 || !b1 || !w2 || !h || !g || !y) return hvk_set_error(HVK_EINVAL, "hvk_mlp_fwd: null pointer");
-  if (!hvk_mlp_fwd_supported(M, K, N1, N2))
-    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_fwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
+}  // extern "C"
+namespace {
+template <bool LN>
+int launch_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                   void* g, void* y, int M, int K, int N1, int N2, const LnEpi& ln, void* stream) {
   constexpr int WAVES = 8;
-  constexpr size_t LDS = kMlpFwdLds;
+  constexpr size_t LDS = kMlpFwdLds + (LN ? (size_t)WAVES * ln96::STAGE_BYTES + ln96::PARAM_BYTES : 0);
   if (!g_cu_count) {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -789,14 +956,74 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
   const int need = (tiles + WAVES - 1) / WAVES;
   if (groups > need) groups = need;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // x in; h, GELU(h), y out (the hidden tensors are written for the backward, never re-read here)
-  hvk_timer_shape("mlp_fwd", 1, WAVES, M, N1, K, 2.0 * M * (K + 2.0 * N1 + N2) + 4.0 * N1 * K);
-  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_fwd_kernel<WAVES>), dim3(groups),
+  // x in; h, GELU(h), y out (the hidden tensors are written for the backward, never re-read here);
+  // LN: + x0 in, x (f32), xb out
+  hvk_timer_shape("mlp_fwd", LN ? 5 : 1, WAVES, M, N1, K,
+                  2.0 * M * (K + 2.0 * N1 + N2) + 4.0 * N1 * K +
+                      (LN ? (ln.x0 ? 4.0 : 0.0) * M * N2 + (ln.xb ? 6.0 : 4.0) * M * N2 + 8.0 * M : 0.0));
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * (double)N1 * K * 2, (mlp_fwd_kernel<WAVES, LN>), dim3(groups),
                      dim3(64 * WAVES), LDS, st, static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w1),
                      b1, static_cast<const hvk_bf16*>(w2), b2, static_cast<hvk_bf16*>(h),
-                     static_cast<hvk_bf16*>(g), static_cast<hvk_bf16*>(y), M, groups);
+                     static_cast<hvk_bf16*>(g), static_cast<hvk_bf16*>(y), M, groups, ln);
   HVK_CHECK_LAUNCH("hvk_mlp_fwd");
   return HVK_OK;
+}
+int g_mlp_ln_lds = 0;
+int check_ln(const char* who, const float* gamma, const float* beta, int rows_per_sample, const float* sscale,
+             float* x_out, float* mean, float* rstd) {
+  if (!gamma || !beta || !x_out || !mean || !rstd) return hvk_set_error(HVK_EINVAL, "%s: null pointer", who);
+  if (sscale && rows_per_sample <= 0) return hvk_set_error(HVK_EINVAL, "%s: rows_per_sample %d", who, rows_per_sample);
+  return HVK_OK;
+}
+}  // namespace
+extern "C" {
+
+int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, const float* b2, void* h,
+                void* g, void* y, int M, int K, int N1, int N2, void* stream) {
+  if (!x || !w1 || !b1 || !w2 || !h || !g || !y) return hvk_set_error(HVK_EINVAL, "hvk_mlp_fwd: null pointer");
+  if (!hvk_mlp_fwd_supported(M, K, N1, N2))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_fwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
+  return launch_mlp_fwd<false>(x, w1, b1, w2, b2, h, g, y, M, K, N1, N2, LnEpi{}, stream);
+}
+
+int hvk_mlp_ln_supported(int M, int K, int N1, int N2) {
+  return M > 0 && K == 96 && N1 == 384 && N2 == 96 &&
+         mlp_lds_granted(reinterpret_cast<const void*>(&mlp_fwd_kernel<8, true>),
+                         kMlpFwdLds + 8 * ln96::STAGE_BYTES + ln96::PARAM_BYTES, g_mlp_ln_lds);
+}
+
+int hvk_mlp_ln_fwd(const void* x, const void* w1, const float* b1, const void* w2, void* h, void* g, void* a_out,
+                   int M, int K, int N1, int N2, const float* abias, const float* x0, const float* gamma,
+                   const float* beta, const float* sample_scale, int rows_per_sample, float eps, float* x_out,
+                   void* xb_out, float* mean, float* rstd, void* stream) {
+  if (!x || !w1 || !b1 || !w2 || !h || !g || !a_out) return hvk_set_error(HVK_EINVAL, "hvk_mlp_ln_fwd: null pointer");
+  int rc = check_ln("hvk_mlp_ln_fwd", gamma, beta, rows_per_sample, sample_scale, x_out, mean, rstd);
+  if (rc) return rc;
+  if (!hvk_mlp_ln_supported(M, K, N1, N2))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_mlp_ln_fwd: shape M=%d K=%d N1=%d N2=%d not built", M, K, N1, N2);
+  const LnEpi ln{abias, x0, gamma, beta, sample_scale, rows_per_sample, eps, x_out, static_cast<hvk_bf16*>(xb_out),
+                 mean, rstd};
+  return launch_mlp_fwd<true>(x, w1, b1, w2, nullptr, h, g, a_out, M, K, N1, N2, ln, stream);
+}
+
+int hvk_linear_ln_supported(int M, int K, int N) { return M > 0 && N == 96 && (K == 96 || K == 48); }
+
+int hvk_linear_ln_fwd(const void* x, const void* w, int M, int K, int N, const float* abias, const float* x0,
+                      const float* gamma, const float* beta, const float* sample_scale, int rows_per_sample,
+                      float eps, void* a_out, float* x_out, void* xb_out, float* mean, float* rstd, void* stream) {
+  if (!x || !w || !a_out) return hvk_set_error(HVK_EINVAL, "hvk_linear_ln_fwd: null pointer");
+  int rc = check_ln("hvk_linear_ln_fwd", gamma, beta, rows_per_sample, sample_scale, x_out, mean, rstd);
+  if (rc) return rc;
+  if (!hvk_linear_ln_supported(M, K, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_linear_ln_fwd: shape M=%d K=%d N=%d not built", M, K, N);
+  const LnEpi ln{abias, x0, gamma, beta, sample_scale, rows_per_sample, eps, x_out, static_cast<hvk_bf16*>(xb_out),
+                 mean, rstd};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
+  const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
+  hvk_bf16* A = static_cast<hvk_bf16*>(a_out);
+  if (K == 96) return launch_linear<96, 96, 8, true, 5>(X, W, nullptr, A, M, N, st, nullptr, nullptr, nullptr, ln);
+  return launch_linear<48, 96, 8, true, 5>(X, W, nullptr, A, M, N, st, nullptr, nullptr, nullptr, ln);
 }
 
 int hvk_mlp_bwd_supported(int M, int K, int N1, int N2) {

@@ -806,23 +806,97 @@ class LayerNormResidual(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, gxb):
         a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
-        C = a.shape[-1]
-        rows = a.numel() // C
-        gx = _f32(gx) if gx is not None else None
-        gxb = _bf16(gxb) if gxb is not None else None
-        if gx is None and gxb is None:
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        if r is None:
             return (None,) * 8
-        ga = torch.empty_like(a)
-        gx0 = torch.empty(a.shape, device=a.device, dtype=torch.float32) if ctx.has_x0 else None
-        dgamma = torch.empty_like(gamma)
-        dbeta = torch.empty_like(gamma)
-        dabias = torch.empty_like(gamma) if abias is not None else None
-        ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
-        ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
-        call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
-             ptr(rstd), ptr(gx), ptr(gxb), rows, C, ctx.rps, ptr(gx0), ptr(ga), ptr(dgamma),
-             ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream())
+        ga, dabias, gx0, dgamma, dbeta = r
         return ga, dabias, gx0, dgamma, dbeta, None, None, None
+
+
+def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx, gxb):
+    """Backward of x = x0 + s (gamma * LN(a + abias) + beta) (hvk_ln_residual_bwd): (ga, dabias,
+    gx0, dgamma, dbeta), or None when neither output has a gradient."""
+    C = a.shape[-1]
+    rows = a.numel() // C
+    gx = _f32(gx) if gx is not None else None
+    gxb = _bf16(gxb) if gxb is not None else None
+    if gx is None and gxb is None:
+        return None
+    ga = torch.empty_like(a)
+    gx0 = torch.empty(a.shape, device=a.device, dtype=torch.float32) if has_x0 else None
+    dgamma = torch.empty_like(gamma)
+    dbeta = torch.empty_like(gamma)
+    dabias = torch.empty_like(gamma) if abias is not None else None
+    ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
+    ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
+    call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
+         ptr(rstd), ptr(gx), ptr(gxb), rows, C, rps, ptr(gx0), ptr(ga), ptr(dgamma),
+         ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream())
+    return ga, dabias, gx0, dgamma, dbeta
+
+
+def _ln_out(a, rows):
+    """Output buffers of a fused post-norm over a's shape: x f32, xb bf16, mean, rstd."""
+    dev = a.device
+    return (torch.empty(a.shape, device=dev, dtype=torch.float32), torch.empty(a.shape, device=dev, dtype=torch.bfloat16),
+            torch.empty(rows, device=dev, dtype=torch.float32), torch.empty(rows, device=dev, dtype=torch.float32))
+
+
+class LinearLNFn(torch.autograd.Function):
+    """(x, xb) = LayerNormResidual(LinearFn(inp, W), abias, x0, ...) with the norm in the GEMM's
+    epilogue (hvk_linear_ln_fwd, C = 96: the stage-0 proj and the patch embedding): one kernel
+    forward instead of two with the same a / x / xb / mean / rstd bits; backward = the LayerNorm
+    backward, then the Linear's (input grad + weight grad, the proj's xshift included)."""
+
+    @staticmethod
+    def forward(ctx, inp, weight, xshift, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        xin = _bf16(inp)
+        wb, wt = _bf16_weight(weight)
+        N, K = wb.shape
+        M = xin.numel() // K
+        a = torch.empty((*xin.shape[:-1], N), device=xin.device, dtype=torch.bfloat16)
+        x, xb, mean, rstd = _ln_out(a, M)
+        gamma, beta = _f32(gamma), _f32(beta)
+        abias = _f32(abias) if abias is not None else None
+        x0 = _f32(x0) if x0 is not None else None
+        sample_scale = _f32(sample_scale) if sample_scale is not None else None
+        call("hvk_linear_ln_fwd", ptr(xin), ptr(wb), M, K, N, ptr(abias), ptr(x0), ptr(gamma), ptr(beta),
+             ptr(sample_scale), rows_per_sample, float(eps), ptr(a), ptr(x), ptr(xb), ptr(mean), ptr(rstd),
+             stream())
+        ctx.save_for_backward(xin, wb, a, abias, gamma, sample_scale, mean, rstd)
+        ctx.wt = wt
+        ctx.xshift = xshift.detach() if xshift is not None else None
+        ctx.has_x0 = x0 is not None
+        ctx.rps = rows_per_sample
+        ctx.set_materialize_grads(False)
+        return x, xb
+
+    @staticmethod
+    def backward(ctx, gx, gxb):
+        xin, wb, a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        if r is None:
+            return (None,) * 10
+        ga, dabias, gx0, dgamma, dbeta = r
+        N, K = wb.shape
+        g2 = ga.reshape(-1, N)
+        gin = None
+        if ctx.needs_input_grad[0]:
+            gin = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K) else g2 @ wb).reshape(xin.shape)
+        dw = weight_grad(g2, xin.reshape(-1, K), False, xshift=ctx.xshift)[0] if ctx.needs_input_grad[1] else None
+        return gin, dw, None, dabias, gx0, dgamma, dbeta, None, None, None
+
+
+def linear_ln_supported(M, K, N):
+    """The fused Linear + post-norm (hvk_linear_ln_fwd) is built for this shape and enabled."""
+    return OPTIONS.ln_epilogue and bool(_lib.load().hvk_linear_ln_supported(M, K, N))
+
+
+def linear_ln(inp, weight, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5, abias=None,
+              xshift=None):
+    """LayerNormResidual(F.linear(inp, weight), x0, ...) with the norm fused into the GEMM's
+    epilogue (callers check linear_ln_supported); xshift as for linear()."""
+    return LinearLNFn.apply(inp, weight, xshift, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps)
 
 
 def layer_norm_residual(a, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5,
@@ -1025,6 +1099,85 @@ class MlpFn(torch.autograd.Function):
                   else gh @ w1b).reshape(xb.shape)
         dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
         return gx, dw1, db1, dw2, db2
+
+
+class MlpLNFn(torch.autograd.Function):
+    """(x, xb) = LayerNormResidual(fc2(GELU(fc1(inp))), abias = fc2's bias, x0, ...) at the stage-0
+    width as ONE kernel forward (hvk_mlp_ln_fwd: the fused MLP with the block's norm2 in its
+    epilogue, bit-identical to hvk_mlp_fwd + hvk_ln_residual_fwd); backward = the LayerNorm
+    backward, then MlpFn's fused chain (fc2's bias gradient is the norm's dabias)."""
+
+    @staticmethod
+    def forward(ctx, inp, w1, b1, w2, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        xin = _bf16(inp)
+        w1b, w1t = _bf16_weight(w1)
+        w2b, w2t = _bf16_weight(w2)
+        N1, K = w1b.shape
+        N2 = w2b.shape[0]
+        x2 = xin.reshape(-1, K)
+        M = x2.shape[0]
+        h = torch.empty((M, N1), device=x2.device, dtype=torch.bfloat16)
+        y1 = torch.empty_like(h)
+        a = torch.empty((*xin.shape[:-1], N2), device=xin.device, dtype=torch.bfloat16)
+        x, xb, mean, rstd = _ln_out(a, M)
+        gamma, beta = _f32(gamma), _f32(beta)
+        abias = _f32(abias) if abias is not None else None
+        x0 = _f32(x0) if x0 is not None else None
+        sample_scale = _f32(sample_scale) if sample_scale is not None else None
+        call("hvk_mlp_ln_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(w2b), ptr(h), ptr(y1), ptr(a), M, K, N1, N2,
+             ptr(abias), ptr(x0), ptr(gamma), ptr(beta), ptr(sample_scale), rows_per_sample, float(eps), ptr(x),
+             ptr(xb), ptr(mean), ptr(rstd), stream())
+        ctx.save_for_backward(xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd)
+        ctx.wts = (w1t, w2t)
+        ctx.has_x0 = x0 is not None
+        ctx.rps = rows_per_sample
+        ctx.set_materialize_grads(False)
+        return x, xb
+
+    @staticmethod
+    def backward(ctx, gx, gxb):
+        xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        if r is None:
+            return (None,) * 11
+        ga, dabias, gx0, dgamma, dbeta = r
+        gin, dw1, db1, dw2 = _mlp_bwd(ga, xin, w1b, w2b, h, y1, ctx.wts, ctx.needs_input_grad[0])
+        return gin, dw1, db1, dw2, dabias, gx0, dgamma, dbeta, None, None, None
+
+
+def _mlp_bwd(gy, xb, w1b, w2b, h, y1, wts, want_x):
+    """MlpFn's backward at the stage-0 width (the fused hvk_mlp_bwd chain; fc2's bias gradient is
+    the caller's): (gx, dW1, db1, dW2)."""
+    N1, K = w1b.shape
+    N2 = w2b.shape[0]
+    g2 = _bf16(gy).reshape(-1, N2)
+    M = g2.shape[0]
+    dw2 = weight_grad(g2, y1)[0]
+    gh = torch.empty_like(h)
+    w2t = _bf16_t(w2b, wts[1])
+    gx = None
+    if want_x:
+        gx = torch.empty((M, K), device=h.device, dtype=torch.bfloat16)
+        call("hvk_mlp_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(_bf16_t(w1b, wts[0])), ptr(gh), ptr(gx), M, N2, N1, K,
+             stream())
+        gx = gx.reshape(xb.shape)
+    else:
+        call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1, stream())
+    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+    return gx, dw1, db1, dw2
+
+
+def mlp_ln_supported(M, K, N1, N2):
+    """The fused MLP + post-norm (hvk_mlp_ln_fwd, and its fused backward chain) applies."""
+    lib = _lib.load()
+    return (OPTIONS.ln_epilogue and OPTIONS.mlp_fused and bool(lib.hvk_mlp_ln_supported(M, K, N1, N2))
+            and bool(lib.hvk_mlp_bwd_supported(M, N2, N1, K)))
+
+
+def mlp_ln(x, w1, b1, w2, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5, abias=None):
+    """LayerNormResidual(fc2(GELU(fc1(x))), x0, ...) with fc2's bias as the norm's abias, one kernel
+    forward (callers check mlp_ln_supported)."""
+    return MlpLNFn.apply(x, w1, b1, w2, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps)
 
 
 def mlp(x, w1, b1, w2, b2=None):

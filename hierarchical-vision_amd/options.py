@@ -29,6 +29,9 @@ class HostOptions:
     norm_pool: bool = True
     # the stage-0 MLP forward / input-gradient chain as one kernel each (hvk_mlp_fwd / _bwd)
     mlp_fused: bool = True
+    # C = 96 (stage 0): the post-norm LayerNorm + residual in the epilogue of the proj / fc2 /
+    # patch-embedding GEMM (hvk_linear_ln_fwd, hvk_mlp_ln_fwd) instead of a separate launch
+    ln_epilogue: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

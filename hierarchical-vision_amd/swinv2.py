@@ -248,10 +248,12 @@ class WindowAttention(nn.Module):
                 self.logit_scale, self.q_bias, self._logit_clamp))
         return self.gemm_biases() + self.cpb_tables()
 
-    def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None):
+    def forward_tokens(self, x, H, W, shift, proj_bias=True, biases=None, core_only=False):
         """x: bf16 [B, H*W, C] un-partitioned tokens -> [B, H*W, C] after proj (without
         proj's bias when proj_bias=False: the caller folds the proj bias into the next
-        kernel).  biases: block_tables() (or gemm_biases()) when the caller already has them."""
+        kernel).  biases: block_tables() (or gemm_biases()) when the caller already has them.
+        core_only: return (o, xshift) -- the attention core's output (proj's input) and the proj
+        weight gradient's xshift -- for a caller that runs proj fused with its post-norm."""
         if biases is None:
             biases = self.block_tables()
         qkv_b, proj_b = biases[:2]
@@ -266,9 +268,10 @@ class WindowAttention(nn.Module):
         # the v_bias share of d proj.weight: from this Linear's weight-gradient kernel exactly when
         # the proj bias came from the fused tables (W_proj detached there); gemm_biases() and the
         # unfused tables route it through autograd already
-        fold = isinstance(biases, ProjFoldTables)
-        return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None,
-                                         xshift=self.v_bias if fold else None))
+        xshift = self.v_bias if isinstance(biases, ProjFoldTables) else None
+        if core_only:
+            return o, xshift
+        return self.proj_drop(ops.linear(o, self.proj.weight, proj_b if proj_bias else None, xshift=xshift))
 
     def forward(self, x, mask=None):
         """Reference API (swinv2.py:204): x = windows [nW*B, N, C]."""
@@ -339,19 +342,32 @@ class SwinTransformerBlock(nn.Module):
         assert L == H * W, "input feature has wrong size"
         fold = self.attn.proj_drop.p == 0 or not self.training  # proj bias -> LN kernel
         biases = self.attn.block_tables()
-        a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold,
-                                     biases=biases)
         planned = getattr(self, "_dp", None) if self.training else None  # from _plan_drop_path
         if planned is not None and planned[0].shape[0] != B:
             planned = None
-        dp = planned[0] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
-        x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
-                                        self.norm1.eps, abias=biases[1] if fold else None)
+        dev = s.f32.device
+        dp = planned[0] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, dev)
+        if fold and s.f32.is_cuda and ops.linear_ln_supported(B * L, C, C):
+            # stage 0: proj + norm1 (+ DropPath + residual) as one kernel (hvk_linear_ln_fwd)
+            o, xshift = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, biases=biases, core_only=True)
+            x, xb = ops.linear_ln(o, self.attn.proj.weight, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
+                                  self.norm1.eps, abias=biases[1], xshift=xshift)
+        else:
+            a = self.attn.forward_tokens(s.bf16, H, W, self.shift_size, proj_bias=not fold, biases=biases)
+            x, xb = ops.layer_norm_residual(a, s.f32, self.norm1.weight, self.norm1.bias, dp, L,
+                                            self.norm1.eps, abias=biases[1] if fold else None)
         fold = self.mlp.drop.p == 0 or not self.training  # fc2 bias -> LN kernel
-        h = self.mlp.forward_tokens(xb, fc2_bias=not fold)
-        dp = planned[1] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, a.device)
+        dp = planned[1] if planned else _drop_path_scale(self.drop_path_prob, self.training, B, dev)
+        m = self.mlp
+        if (fold and x.is_cuda and isinstance(m.act, nn.GELU) and m.act.approximate == "none"
+                and m.fc1.bias is not None
+                and ops.mlp_ln_supported(B * L, C, m.fc1.out_features, m.fc2.out_features)):
+            # stage 0: fc1 + GELU + fc2 + norm2 (+ DropPath + residual) as one kernel (hvk_mlp_ln_fwd)
+            return ResidualStream(*ops.mlp_ln(xb, m.fc1.weight, m.fc1.bias, m.fc2.weight, x, self.norm2.weight,
+                                              self.norm2.bias, dp, L, self.norm2.eps, abias=m.fc2.bias))
+        h = m.forward_tokens(xb, fc2_bias=not fold)
         x, xb = ops.layer_norm_residual(h, x, self.norm2.weight, self.norm2.bias, dp, L,
-                                        self.norm2.eps, abias=self.mlp.fc2.bias if fold else None)
+                                        self.norm2.eps, abias=m.fc2.bias if fold else None)
         return ResidualStream(x, xb)
 
     def forward(self, x):
@@ -503,6 +519,11 @@ class PatchEmbed(nn.Module):
         w = self.proj.weight.reshape(self.embed_dim, -1)
         if self.norm is None:
             return _as_stream(ops.linear(patches, w, self.proj.bias))
+        if (isinstance(self.norm, nn.LayerNorm) and patches.is_cuda
+                and ops.linear_ln_supported(patches.numel() // w.shape[1], w.shape[1], w.shape[0])):
+            # the embedding GEMM with its LayerNorm in the epilogue (hvk_linear_ln_fwd, plain norm)
+            return ResidualStream(*ops.linear_ln(patches, w, None, self.norm.weight, self.norm.bias, None, 1,
+                                                 self.norm.eps, abias=self.proj.bias))
         y = ops.linear(patches, w)
         x32, x16 = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1,
                                            self.norm.eps, abias=self.proj.bias)

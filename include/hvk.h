@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 /* the C ABI this header describes; hvk_abi_version() returns it (bindings check it at load) */
-#define HVK_ABI_VERSION 10
+#define HVK_ABI_VERSION 11
 
 #define HVK_OK 0
 #define HVK_EINVAL 1
@@ -180,6 +180,23 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
  * weight gradient reads it); bit-identical to hvk_linear_gelu_bwd + hvk_linear_fwd(gh, w1t)
  * without the second kernel's re-read of gh.  gy [M, 96], w2t = fc2.weight^T [384, 96],
  * h [M, 384], w1t = fc1.weight^T [96, 384]; gh [M, 384], gx [M, 96]. */
+/* The post-norm LayerNorm + residual of swinv2.py:431 / 434 (and PatchEmbed's plain norm, 656)
+ * fused into the producing GEMM's epilogue at C = 96 (SwinV2-T stage 0), replacing the Linear
+ * (run without its bias) + hvk_ln_residual_fwd pair: a = bf16(x W^T) is stored (the LayerNorm
+ * backward reads it) and x = x0 + s[b] (gamma (a + abias - mean) rstd + beta), xb = bf16(x), mean,
+ * rstd come out of the same pass, bit-identical to hvk_ln_residual_fwd on that a (same lane layout
+ * and arithmetic).  x0 NULL: plain norm; sample_scale NULL: no DropPath; xb_out NULL: not stored.
+ * linear: N = 96 with K = 96 (proj) or K = 48 (the patch embedding); mlp: the hvk_mlp_fwd shape with
+ * the fc2 output normalised (fc2's bias passed as abias).  ABI 11. */
+int hvk_linear_ln_supported(int M, int K, int N);
+int hvk_linear_ln_fwd(const void* x, const void* w, int M, int K, int N, const float* abias, const float* x0,
+                      const float* gamma, const float* beta, const float* sample_scale, int rows_per_sample,
+                      float eps, void* a_out, float* x_out, void* xb_out, float* mean, float* rstd, void* stream);
+int hvk_mlp_ln_supported(int M, int K, int N1, int N2);
+int hvk_mlp_ln_fwd(const void* x, const void* w1, const float* b1, const void* w2, void* h, void* g, void* a_out,
+                   int M, int K, int N1, int N2, const float* abias, const float* x0, const float* gamma,
+                   const float* beta, const float* sample_scale, int rows_per_sample, float eps, float* x_out,
+                   void* xb_out, float* mean, float* rstd, void* stream);
 int hvk_mlp_bwd_supported(int M, int K, int N1, int N2);
 int hvk_mlp_bwd(const void* gy, const void* w2t, const void* h, const void* w1t, void* gh, void* gx, int M,
                 int K, int N1, int N2, void* stream);
