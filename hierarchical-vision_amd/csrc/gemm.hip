@@ -151,11 +151,11 @@ __device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t s
     for (int i = 0; i < NG; ++i)
       if (grp_ok(t, i)) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { const float d = v[4 * i + j] - mu; ss += d * d; }
+        for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
       }
 #pragma unroll
     for (int m = TPR / 2; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
-    const float rs = rsqrtf(ss * invC + p.eps);
+    const float rs = hvk_ln_rstd(ss, invC, p.eps);
     if (row >= M) continue;
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
     const size_t rb = (size_t)row * C;
@@ -168,7 +168,7 @@ __device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t s
       const float4 g4 = param4(q, 0, c), b4 = param4(q, 1, c);
       const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] += ((v[4 * i + j] - mu) * rs * gm[j] + bt[j]) * sc;
+      for (int j = 0; j < 4; ++j) r[j] = hvk_ln_out(r[j], v[4 * i + j], mu, rs, gm[j], bt[j], sc);
       const uint4 xr = make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3]));
       if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
       else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;

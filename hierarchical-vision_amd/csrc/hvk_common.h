@@ -127,6 +127,20 @@ __device__ __forceinline__ uint4 hvk_pack8(const float f[8]) {
                     hvk_pack2(f[6], f[7]));
 }
 
+// ---- post-norm LayerNorm arithmetic, pinned op by op ---------------------------------------
+// ln_fwd_kernel (layernorm.hip) and the GEMM epilogues that reproduce it bit for bit (gemm.hip,
+// ln96) share these: left to the contraction pass, the SLP vectoriser turned `ss += d * d` into
+// v_pk_mul_f32 + v_add_f32 in one kernel and v_pk_fma_f32 in the other (rstd 1-2 ulp apart in
+// ~5 % of rows); explicit fmas round the same wherever they are vectorised.
+__device__ __forceinline__ float hvk_ln_sq(float ss, float d) { return __builtin_fmaf(d, d, ss); }
+__device__ __forceinline__ float hvk_ln_rstd(float ss_row, float invC, float eps) {
+  return rsqrtf(__builtin_fmaf(ss_row, invC, eps));
+}
+// x0 + (gamma (v - mu) rstd + beta) * sc
+__device__ __forceinline__ float hvk_ln_out(float x0, float v, float mu, float rs, float gm, float bt, float sc) {
+  return __builtin_fmaf(__builtin_fmaf((v - mu) * rs, gm, bt), sc, x0);
+}
+
 // ---- 16-B / 8-B global access with an optional nontemporal hint ------------------------
 // The nontemporal hint gains +14 % on a full-line 3:1 read:write stream on gfx950 but LOSES
 // 24 % on the W-MSA access shape (64-B row segments whose line halves belong to another

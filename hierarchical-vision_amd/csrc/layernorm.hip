@@ -125,9 +125,9 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
     for (int i = 0; i < NG; ++i)
       if (ok[i]) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { const float d = v[4 * i + j] - mu; ss += d * d; }
+        for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
       }
-    const float rs = rsqrtf(group_sum<TPR>(ss) * invC + p.eps);
+    const float rs = hvk_ln_rstd(group_sum<TPR>(ss), invC, p.eps);
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64 * kWaves) void ln_fwd_kernel(LnFwd p) {
         ld4_f32_stream(p.x0 + rb + c, r);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] += ((v[4 * i + j] - mu) * rs * gm[4 * i + j] + bt[4 * i + j]) * sc;
+      for (int j = 0; j < 4; ++j) r[j] = hvk_ln_out(r[j], v[4 * i + j], mu, rs, gm[4 * i + j], bt[4 * i + j], sc);
       st4_f32(p.x + rb + c, r, HVK_NT_SAVED & 2);  // the f32 stream is read again only at the next LayerNorm
       if (p.xb) st4_bf16(p.xb + rb + c, r);
     }

@@ -7,7 +7,8 @@ reference network in f32 there.  Bounds are derived from the reference itself: t
 CPU bf16-autocast error on that tensor) relative L2 (stored per tensor in the fixture, measured
 on the full tensors; base 5e-2 for the logit-scale and CPB-MLP gradients, sums of dS cos / dS
 that cancel through the bf16 softmax, as in test_gpu_model.py's mini-model bound), all
-gradients together within 2e-2.  HXE is not implemented by the
+gradients together within max(2e-2, the reference's own bf16-autocast error on the same sampled
+elements, estimated from its per-tensor errors: t_hxe 0.028, b224_mt 0.020, b384_hxe 0.035).  HXE is not implemented by the
 reference (hierarchy.py:183-185): the fixture's loss on the reference's logits is the oracle's
 HXE, itself pinned by closed-form tests (tests/test_host_cpu.py)."""
 import numpy as np
@@ -78,7 +79,13 @@ def test_train_step_vs_reference(golden, name):
             bad[k] = (r, lim)
     worst.sort(reverse=True)
     allrel = _rel(np.concatenate(mine), np.concatenate(theirs))
-    print(f"{name}: loss {loss.item():.6f} vs {ref:.6f} (ref bf16 {ref16:.6f}); all grads {allrel:.4f}; "
+    # the reference's own all-gradient bf16 error on these samples: its per-tensor errors weighted
+    # by the sampled norms (sqrt(sum (e16_k |b_k|)^2) / |b|)
+    e16 = [float(g[f"{name}.e16.{k}"]) for k, _ in net.named_parameters()]
+    ref_all16 = float(np.sqrt(sum((e * np.linalg.norm(b)) ** 2 for e, b in zip(e16, theirs)))
+                      / np.linalg.norm(np.concatenate(theirs)))
+    print(f"{name}: loss {loss.item():.6f} vs {ref:.6f} (ref bf16 {ref16:.6f}); all grads {allrel:.4f} "
+          f"(reference's own bf16 {ref_all16:.4f}); "
           f"closest to bound (r/lim, r, lim): {[(round(u, 2), round(v, 4), round(w, 4), k) for u, v, w, k in worst[:6]]}")
     assert not bad, bad
-    assert allrel < BASE, allrel
+    assert allrel < max(BASE, ref_all16), (allrel, ref_all16)
