@@ -183,7 +183,9 @@ __device__ void build_bounded_table(float* tab, float* wmax, const float* __rest
 
 #ifdef HVK_STAMPS
 // diagnostic build (tools/bwd_stamps.py): per-phase shader-clock sums over all waves
-__device__ unsigned long long g_bwd_stamps[8];
+// [0..6] window-loop phases, [7] waves, [8] setup (entry -> loop), [9] teardown (loop -> exit;
+// includes draining the phase stamps' own contended atomics), [10] / [11] unused (per-XCD clocks)
+__device__ unsigned long long g_bwd_stamps[12];
 #define BSTAMP(k)                                             \
   do {                                                        \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -208,6 +210,9 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   int w0, w1;
   chunk_range(g, chunk, w0, w1);
   if (w0 >= w1) return;
+#ifdef HVK_STAMPS
+  const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
+#endif
 
   // wave-uniform in SGPRs: the window index, its coordinates and edge flags stay scalar
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -314,6 +319,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 #ifdef HVK_STAMPS
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_acc_setup = st_prev - st_entry;
 #endif
 
   for (int it = 0; it < n_iter; ++it) {
@@ -565,6 +571,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   if (lane == 0)
     for (int k = 0; k < 7; ++k) atomicAdd(&g_bwd_stamps[k], st_acc[k]);
   if (lane == 0) atomicAdd(&g_bwd_stamps[7], 1ull);
+  const unsigned long long st_loop_end = __builtin_amdgcn_s_memtime();
 #endif
 
   // ---- workgroup reduction of the bias / scale gradients (carried as scale*dS), then one
@@ -598,6 +605,13 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       const float v = hvk_row16_sum(dqb[dt][r]);
       if (li == 0) atomicAdd(a.dqb_acc + h * 32 + 16 * dt + 4 * gq + r, v);
     }
+#ifdef HVK_STAMPS
+  __syncthreads();
+  if (lane == 0) {
+    atomicAdd(&g_bwd_stamps[8], st_acc_setup);
+    atomicAdd(&g_bwd_stamps[9], __builtin_amdgcn_s_memtime() - st_loop_end);
+  }
+#endif
 }
 
 // Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R], write
@@ -687,9 +701,9 @@ extern "C" {
 
 #ifdef HVK_STAMPS
 int hvk_debug_bwd_stamps(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamps), 8 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamps), 12 * sizeof(unsigned long long)) != hipSuccess)
     return HVK_EINVAL;
-  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_stamps), z, sizeof(z)) == hipSuccess ? HVK_OK : HVK_EINVAL;
 }
 #endif

@@ -7,13 +7,16 @@
 set -e
 REV=$1; NAME=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-T=$(mktemp -d /tmp/hvkvar.XXXX)
-if [ "$REV" = WT ]; then cp -r "$ROOT/hierarchical-vision_amd/csrc/." "$T/"; rm -rf "$T/build"
-else git -C "$ROOT" archive "$REV" hierarchical-vision_amd/csrc | tar -x -C "$T" --strip-components=2; fi
+TT=$(mktemp -d /tmp/hvkvar.XXXX)
+T=$TT/pkg/csrc  # csrc/../../include/hvk.h as in the tree
+mkdir -p "$T" "$TT/include"
+if [ "$REV" = WT ]; then cp -r "$ROOT/hierarchical-vision_amd/csrc/." "$T/"; rm -rf "$T/build"; cp "$ROOT/include/hvk.h" "$TT/include/"
+else git -C "$ROOT" archive "$REV" hierarchical-vision_amd/csrc | tar -x -C "$T" --strip-components=2
+  git -C "$ROOT" show "$REV:include/hvk.h" > "$TT/include/hvk.h"; fi
 for fr in $FROM_REV; do
   git -C "$ROOT" show "${fr%%:*}:hierarchical-vision_amd/csrc/${fr#*:}" > "$T/${fr#*:}"
 done
 mkdir -p "$ROOT/abl"
 make -s -C "$T" -j8 OUT="$ROOT/abl/$NAME.so" CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result $EXTRA"
-rm -rf "$T"
+rm -rf "$TT"
 echo "built abl/$NAME.so"

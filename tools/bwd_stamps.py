@@ -27,7 +27,7 @@ def main():
     scale = torch.full((nh,), 10.0, device="cuda", requires_grad=True)
     g = torch.randn(B, H * W, C, device="cuda").bfloat16()
     lib = ctypes.CDLL(os.environ["HVK_LIB_PATH"])
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 12)()
     for it in range(3):
         out = ops.window_attention_core(qkv, tab, scale, H, W, nh, win, shift)
         torch.cuda.synchronize()
@@ -40,6 +40,8 @@ def main():
     print(f"{name}: {waves} waves, {tot / waves:.0f} cycles per wave in the window loop")
     for k, p in enumerate(PHASES):
         print(f"  {p:40s} {buf[k] / waves:10.0f} cyc/wave  {100 * buf[k] / tot:5.1f} %")
+    print(f"  setup (entry -> loop)                    {buf[8] / waves:10.0f} cyc/wave")
+    print(f"  teardown (loop -> exit)                  {buf[9] / waves:10.0f} cyc/wave")
 
 
 if __name__ == "__main__":
