@@ -389,22 +389,37 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
         }
         const int q = 16 * qi + li;
         const float* tq = btab + (qi * NT * 64 + lane) * 4;
-        const uint32_t mm = (edge_r || edge_c) ? mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c) : 0u;
+        const bool edge = edge_r || edge_c;  // wave-uniform
+        const uint32_t mm = edge ? mask_bits(krow, kcol, q, WIN - g.shift, WIN, edge_r, edge_c) : 0u;
         float p[NT][4];
         float sum = 0.f, du = 0.f;
+        float x[NT][4];
 #pragma unroll
         for (int ki = 0; ki < NT; ++ki) {
           const float4 bb = *reinterpret_cast<const float4*>(tq + ki * 256);
           const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
+          for (int r = 0; r < 4; ++r) x[ki][r] = NORMED ? s[ki][r] + bv[r] : fmaf(s[ki][r], sc2, bv[r]);  // NORMED: s = q^ sc2 . k^
+        }
+        // the -100 mask of an edge window in a branch of its own (interior windows and unshifted
+        // blocks skip it): as a select per score on the uniform edge flag it cost 5 VALU each, a
+        // third of the tile's VALU; mm opaque so its bit conversions stay inside the branch
+        if (edge) {
+          uint32_t m1 = mm;
+          asm volatile("" : "+v"(m1));
+#pragma unroll
+          for (int ki = 0; ki < NT; ++ki)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[ki][r] = fmaf((float)((m1 >> (ki * 4 + r)) & 1u), mask2, x[ki][r]);
+        }
+#pragma unroll
+        for (int ki = 0; ki < NT; ++ki)
+#pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = NORMED ? s[ki][r] + bv[r] : fmaf(s[ki][r], sc2, bv[r]);  // NORMED: s = q^ sc2 . k^
-            if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
-            p[ki][r] = __builtin_amdgcn_exp2f(x);
+            p[ki][r] = __builtin_amdgcn_exp2f(x[ki][r]);
             sum += p[ki][r];
             du = fmaf(p[ki][r], dp[ki][r], du);
           }
-        }
         sum = hvk_group4_sum(sum);
         if (__builtin_expect(__ballot(sum < 0x1p-100f) != 0, 0)) {
           // a row whose every logit sits far below the head bound (zero query vector):
@@ -417,7 +432,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float x = NORMED ? s[ki][r] + bv[r] : fmaf(s[ki][r], sc2, bv[r]);  // NORMED: s = q^ sc2 . k^
-              if (edge_r || edge_c) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
+              if (edge) x += ((mm >> (ki * 4 + r)) & 1u) ? mask2 : 0.f;
               p[ki][r] = x;
               mx = fmaxf(mx, x);
             }
