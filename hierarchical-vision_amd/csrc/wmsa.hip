@@ -36,6 +36,9 @@ constexpr int kWaves = 4;
 #ifndef HVK_BWD_PROBE  // tools/ timing probes of the w <= 8 backward (results wrong when set)
 #define HVK_BWD_PROBE 0
 #endif
+#ifndef HVK_BWD_EARLY  // 1: the next window's own q / k / dO rows issued at the top (A/B build switch)
+#define HVK_BWD_EARLY 1
+#endif
 #ifndef HVK_BWD_PF  // 1: next window's inputs loaded under phase B (see wmsa_bwd_kernel)
 #define HVK_BWD_PF 1
 #endif
@@ -272,26 +275,30 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   float dscale = 0.f;
   float dqb[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 
-  // own q, k, dO tiles and all V tiles of a window -> registers (next window: issued after
-  // phase A into the registers phase A was the last to read, so the loads hide under phase B)
+  // own q, k, dO tiles and all V tiles of a window -> registers.  HVK_BWD_EARLY: the next
+  // window's own q, k, dO rows are issued at the top, right after this window's were written to
+  // the LDS images (phase A reads its q / dO fragments back from there), so they land under
+  // phases A and B; its V tiles, which phase A reads from registers, after phase A.
   // qkv reads (the saved activation, read once here): nontemporal when QNT, so a qkv larger
   // than the Infinity Cache does not evict dO and the dqkv this kernel writes for the next GEMMs
   auto qld = [&](uint32_t off) { return QNT ? hvk_bld16_nt(r_qkv, off) : hvk_bld16(r_qkv, off); };
   uint4 qf[TPW], kf[TPW], df[TPW], vf[NT];
   int rown[TPW];  // own token rows of the next window, -1 = padding
-  auto load_window = [&](int w) {
+  // token rows of window w (recomputed per load, not hoisted into registers that would spill:
+  // a spill reload would wait (vmcnt) for every store left in flight)
+  auto token_rows = [&](int w, int (&rt)[NT]) {
     const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
-    // recomputed per window, not hoisted into registers that would spill: a spill reload
-    // here would wait (vmcnt) for every store phase A left in flight
     int lw = li;
     asm volatile("" : "+v"(lw));
-    int rt[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int tok = 16 * t + lw;
       rt[t] = tok < K::N ? window_token_row(g, b, wh, ww, WIN, tok) : -1;
-      vf[t] = qld(rt[t] < 0 ? HVK_OOB : (uint32_t)(rt[t] * C3 + 2 * C + h * 32 + 8 * gq) * 2);
     }
+  };
+  auto load_tiles = [&](int w) {
+    int rt[NT];
+    token_rows(w, rt);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) {
       rown[j] = 2 * j + 1 < NT ? (hf ? rt[2 * j + 1] : rt[2 * j]) : (hf ? -1 : rt[2 * j]);
@@ -302,10 +309,20 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       df[j] = hvk_bld16(r_dout, od);
     }
   };
+  auto load_v = [&](int w) {
+    int rt[NT];
+    token_rows(w, rt);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      vf[t] = qld(rt[t] < 0 ? HVK_OOB : (uint32_t)(rt[t] * C3 + 2 * C + h * 32 + 8 * gq) * 2);
+  };
   // every wave runs the same number of iterations (the barriers are workgroup-wide); a pair
   // without a window in the last one only joins the barriers
   const int n_iter = (w1 - w0 + 1) / 2;
-  if (w0 + pair < w1) load_window(w0 + pair);
+  if (w0 + pair < w1) {
+    load_v(w0 + pair);
+    load_tiles(w0 + pair);
+  }
   // phase B's dK / dV stores leave at the top of the NEXT iteration, after the waits for the
   // prefetched loads: in flight behind those loads they would be drained by the waits
   // (vmcnt counts loads and stores in issue order)
@@ -357,6 +374,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       hvk_bst16(r_dqkv, st_off[j], st_k[j]);
       hvk_bst16(r_dqkv, st_off[j] + 2 * C, st_v[j]);
     }
+    if (HVK_BWD_EARLY && w + 2 < w1) load_tiles(w + 2);  // into the registers just written to LDS
     BSTAMP(0);      // loads landed, normalised, images written
     lds_barrier();  // the pair's q^, k^, dO images complete
     BSTAMP(1);
@@ -382,10 +400,13 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
         if (qi >= NT) break;
         __builtin_amdgcn_sched_barrier(0);  // one query tile's live set at a time
         hvk_f32x4 s[NT], dp[NT];
+        // the own q / dO tile: from the image when the registers already hold the next window's
+        const uint4 qa = HVK_BWD_EARLY ? *reinterpret_cast<const uint4*>(qsb + o_row + 1024 * qi) : qf[j];
+        const uint4 da = HVK_BWD_EARLY ? *reinterpret_cast<const uint4*>(dob + o_row + 1024 * qi) : df[j];
 #pragma unroll
         for (int ki = 0; ki < NT; ++ki) {
-          s[ki] = hvk_mfma16(kfa[ki], qf[j], hvk_f32x4{0, 0, 0, 0});  // cos(q, k)
-          dp[ki] = hvk_mfma16(vf[ki], df[j], hvk_f32x4{0, 0, 0, 0});  // dO . V
+          s[ki] = hvk_mfma16(kfa[ki], qa, hvk_f32x4{0, 0, 0, 0});  // cos(q, k)
+          dp[ki] = hvk_mfma16(vf[ki], da, hvk_f32x4{0, 0, 0, 0});  // dO . V
         }
         const int q = 16 * qi + li;
         const float* tq = btab + (qi * NT * 64 + lane) * 4;
@@ -512,7 +533,10 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       }
     }
     BSTAMP(2);
-    if (w + 2 < w1) load_window(w + 2);
+    if (w + 2 < w1) {
+      load_v(w + 2);  // phase A was the last reader of vf
+      if (!HVK_BWD_EARLY) load_tiles(w + 2);
+    }
     BSTAMP(3);
     lds_barrier();  // P / dS images complete
     BSTAMP(4);
