@@ -20,6 +20,7 @@
 #include <stdlib.h>
 
 #include "hvk_common.h"
+#include "gemm_xr.h"
 
 namespace {
 
@@ -62,19 +63,7 @@ __device__ __forceinline__ int perm_row(int p) {
 // ln_fwd_kernel<8, 16>'s lane layout (layernorm.hip: 16 lanes per row, channel groups of 4 at
 // 4 (16 i + t)) and runs that kernel's arithmetic on it, so x, xb, mean and rstd are bit-identical
 // to the two-launch path (tests/test_gpu_linear_ln.py).
-struct LnEpi {
-  const float* abias;   // [96] the Linear's bias, added in f32 inside the norm (or null)
-  const float* x0;      // [M, 96] f32 residual stream (null: plain norm)
-  const float* gamma;   // [96]
-  const float* beta;    // [96]
-  const float* sscale;  // [M / rows_per_sample] DropPath factor per sample (or null)
-  int rows_per_sample;
-  float eps;
-  float* x;             // [M, 96] f32 out
-  hvk_bf16* xb;         // [M, 96] bf16 copy (next GEMM operand) or null
-  float* mean;          // [M]
-  float* rstd;          // [M]
-};
+// LnEpi (hvk_common.h): the norm's parameters and outputs
 namespace ln96 {
 constexpr int C = 96, TPR = 16, NG = 2, EPT = 8, STAGE_BYTES = 4 * C * 2;
 constexpr int PARAM_BYTES = 3 * C * 4;
@@ -1006,7 +995,10 @@ int hvk_mlp_ln_fwd(const void* x, const void* w1, const float* b1, const void* w
   return launch_mlp_fwd<true>(x, w1, b1, w2, nullptr, h, g, a_out, M, K, N1, N2, ln, stream);
 }
 
-int hvk_linear_ln_supported(int M, int K, int N) { return M > 0 && N == 96 && (K == 96 || K == 48); }
+// C = 96: the skinny kernel (K 96 / 48); C = 192: the 128 x 192 tile kernel (K % 64 == 0)
+int hvk_linear_ln_supported(int M, int K, int N) {
+  return M > 0 && ((N == 96 && (K == 96 || K == 48)) || hvk_tile_ln::supported(M, N, K));
+}
 
 int hvk_linear_ln_fwd(const void* x, const void* w, int M, int K, int N, const float* abias, const float* x0,
                       const float* gamma, const float* beta, const float* sample_scale, int rows_per_sample,
@@ -1022,6 +1014,7 @@ int hvk_linear_ln_fwd(const void* x, const void* w, int M, int K, int N, const f
   const hvk_bf16* X = static_cast<const hvk_bf16*>(x);
   const hvk_bf16* W = static_cast<const hvk_bf16*>(w);
   hvk_bf16* A = static_cast<hvk_bf16*>(a_out);
+  if (N != 96) return hvk_tile_ln::launch(X, W, A, M, N, K, ln, st);
   if (K == 96) return launch_linear<96, 96, 8, true, 5>(X, W, nullptr, A, M, N, st, nullptr, nullptr, nullptr, ln);
   return launch_linear<48, 96, 8, true, 5>(X, W, nullptr, A, M, N, st, nullptr, nullptr, nullptr, ln);
 }

@@ -272,6 +272,99 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
   }
 }
 
+// EPI 5 (N = C = 192: a 128 x 192 tile is whole rows, stage 1): the res-post-norm LayerNorm +
+// residual of swinv2.py:431 / 434 on the staged output image (the tile's `a`, already stored for
+// the norm's backward), in ln_fwd_kernel<8, 32>'s lane layout (32 lanes per row, channel groups
+// of 4 at 4 (32 i + t); layernorm.hip) with its arithmetic (hvk_ln_*), so x, xb, mean and rstd
+// are bit-identical to the two-launch path (tests/test_gpu_linear_ln.py).  A wave takes 2 rows a
+// pass, 16 passes per tile; the next pass's residual rows are loaded under this pass's math.
+namespace ln192 {
+constexpr int C = 192, PASSES = BM / 8;
+__device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int m0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = lane & 31, sub = lane >> 5;
+  const bool ok1 = t < 16;  // group 1 (channels 128 + 4t ..) exists for t < 16
+  float gm[8], bt[8], ab[8];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = 4 * (32 * i + t);
+    float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f), b4 = g4, a4 = g4;
+    if (i == 0 || ok1) {
+      g4 = *reinterpret_cast<const float4*>(p.gamma + c);
+      b4 = *reinterpret_cast<const float4*>(p.beta + c);
+      if (p.abias) a4 = *reinterpret_cast<const float4*>(p.abias + c);
+    }
+    gm[4 * i] = g4.x; gm[4 * i + 1] = g4.y; gm[4 * i + 2] = g4.z; gm[4 * i + 3] = g4.w;
+    bt[4 * i] = b4.x; bt[4 * i + 1] = b4.y; bt[4 * i + 2] = b4.z; bt[4 * i + 3] = b4.w;
+    ab[4 * i] = a4.x; ab[4 * i + 1] = a4.y; ab[4 * i + 2] = a4.z; ab[4 * i + 3] = a4.w;
+  }
+  const float invC = 1.f / C;
+  auto ld_x0 = [&](int pass, float4 (&d)[2]) {
+    const int row = m0 + 8 * pass + 2 * wave + sub;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      d[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.x0 && row < M && (i == 0 || ok1))
+        d[i] = *reinterpret_cast<const float4*>(p.x0 + (size_t)row * C + 4 * (32 * i + t));
+    }
+  };
+  float4 xn[2];
+  ld_x0(0, xn);
+  for (int pass = 0; pass < PASSES; ++pass) {
+    const float4 xc[2] = {xn[0], xn[1]};
+    if (pass + 1 < PASSES) ld_x0(pass + 1, xn);
+    const int r = 8 * pass + 2 * wave + sub, row = m0 + r;
+    float v[8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 0 || ok1) {
+        const int c = 4 * (32 * i + t);
+        const uint2 u = *reinterpret_cast<const uint2*>(img + stage_off<C>(r, c >> 3) + ((c & 7) << 1));
+        v[4 * i] = hvk_lo(u.x); v[4 * i + 1] = hvk_hi(u.x); v[4 * i + 2] = hvk_lo(u.y); v[4 * i + 3] = hvk_hi(u.y);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[4 * i + j] += ab[4 * i + j]; s += v[4 * i + j]; }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    const float mu = s * invC;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (i == 0 || ok1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
+      }
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+    const float rs = hvk_ln_rstd(ss, invC, p.eps);
+    if (row >= M) continue;
+    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
+    const size_t rb = (size_t)row * C;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (!(i == 0 || ok1)) continue;
+      const int c = 4 * (32 * i + t);
+      float o[4] = {xc[i].x, xc[i].y, xc[i].z, xc[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = hvk_ln_out(o[j], v[4 * i + j], mu, rs, gm[4 * i + j], bt[4 * i + j], sc);
+      const uint4 xr = make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+      if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
+      else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
+      if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(o[0], o[1]), hvk_pack2(o[2], o[3]));
+    }
+    if (t == 0) {
+      p.mean[row] = mu;
+      p.rstd[row] = rs;
+    }
+  }
+}
+}  // namespace ln192
+
 template <int EPI, bool PIPE, int TN>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
                                                         const hvk_bf16* __restrict__ Wt,
@@ -279,7 +372,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
                                                         hvk_bf16* __restrict__ Y,
                                                         hvk_bf16* __restrict__ Y2, int M, int N,
                                                         int K, int mtiles, float* __restrict__ rn,
-                                                        const float* __restrict__ qscale) {
+                                                        const float* __restrict__ qscale, LnEpi ln) {
   using T = TileCfg<TN>;
   constexpr int BN = T::BN, STAGE_BYTES = T::STAGE, TILE_BYTES = T::WTILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -421,8 +514,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   const unsigned long long t2 = wall_clock64();
 #endif
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
-  tile_epilogue<EPI, TN, 4, HPB, HVK_TILE_STAGED ? BN : 0>(acc, bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre,
-                                                         rn, qscale, smem, m0, n0);
+  // EPI 5: `a` leaves as EPI 0 (no bias: it is the norm's abias), then the norm of the image
+  static_assert(EPI != 5 || (HVK_TILE_STAGED && TN == 6), "EPI 5 runs on the staged 128 x 192 image");
+  tile_epilogue<EPI == 5 ? 0 : EPI, TN, 4, HPB, HVK_TILE_STAGED ? BN : 0>(acc, EPI == 5 ? nullptr : bias, Y, Y2, M, N,
+                                                                      m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn,
+                                                                      qscale, smem, m0, n0);
+  if constexpr (EPI == 5) ln192::rows(smem, ln, M, m0);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const unsigned long long t3 = wall_clock64();
@@ -622,7 +719,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const hvk_bf16* __restr
 // writes GELU(h), EPI 2 reads h, EPI 4 writes 1/||.|| per token and q / k head (f32)
 double tile_bytes(int epi, double M, double N, double K) {
   return 2.0 * (M * K + N * K + M * N) + (epi == 1 || epi == 2 ? 2.0 * M * N : 0.0) +
-         (epi == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0);
+         (epi == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0) +
+         (epi == 5 ? 10.0 * M * N + 8.0 * M : 0.0);  // EPI 5: x0 in, x + xb out, mean / rstd (x0 counted)
 }
 
 template <int EPI, int WTM, int WTN>
@@ -663,7 +761,8 @@ int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16*
 
 template <int EPI, bool PIPE, int TN>
 int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-                 int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr) {
+                 int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr,
+                 const LnEpi& ln = LnEpi{}) {
   using T = TileCfg<TN>;
   static bool attr = false;
   if (!attr) {
@@ -676,7 +775,7 @@ int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf
   const dim3 grid(mpad * (N / T::BN));
   hvk_timer_shape("gemm_nt", EPI, T::BN, M, N, K, tile_bytes(EPI, M, N, K));
   HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
-                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale);
+                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale, ln);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }
@@ -721,6 +820,15 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
 }
 
 }  // namespace
+
+extern "C" int hvk_gemm_supported(int M, int K, int N);
+namespace hvk_tile_ln {
+bool supported(int M, int N, int K) { return N == ln192::C && hvk_gemm_supported(M, K, N); }
+int launch(const hvk_bf16* X, const hvk_bf16* W, hvk_bf16* Y, int M, int N, int K, const LnEpi& ln, hipStream_t st) {
+  if (!supported(M, N, K)) return hvk_set_error(HVK_EUNSUPPORTED, "tile LN epilogue: M=%d K=%d N=%d", M, K, N);
+  return launch_tile_<5, true, 6>(X, W, nullptr, Y, nullptr, M, N, K, st, nullptr, nullptr, ln);
+}
+}  // namespace hvk_tile_ln
 
 extern "C" {
 

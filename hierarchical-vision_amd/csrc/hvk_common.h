@@ -127,6 +127,23 @@ __device__ __forceinline__ uint4 hvk_pack8(const float f[8]) {
                     hvk_pack2(f[6], f[7]));
 }
 
+// The res-post-norm `x = x0 + drop_path(norm(a))` of swinv2.py:431 / 434 (the plain norm of
+// PatchEmbed, 656, with no x0) applied in a GEMM epilogue whose workgroup holds whole C-wide rows
+// (gemm.hip: C = 96, linear_kernel / mlp_fwd_kernel EPI 5; gemm_tile.hip: C = 192, EPI 5)
+struct LnEpi {
+  const float* abias;   // [C] the Linear's bias, added in f32 inside the norm (or null)
+  const float* x0;      // [M, C] f32 residual stream (null: plain norm)
+  const float* gamma;   // [C]
+  const float* beta;    // [C]
+  const float* sscale;  // [M / rows_per_sample] DropPath factor per sample (or null)
+  int rows_per_sample;
+  float eps;
+  float* x;             // [M, C] f32 out
+  hvk_bf16* xb;         // [M, C] bf16 copy (next GEMM operand) or null
+  float* mean;          // [M]
+  float* rstd;          // [M]
+};
+
 // ---- post-norm LayerNorm arithmetic, pinned op by op ---------------------------------------
 // ln_fwd_kernel (layernorm.hip) and the GEMM epilogues that reproduce it bit for bit (gemm.hip,
 // ln96) share these: left to the contraction pass, the SLP vectoriser turned `ss += d * d` into

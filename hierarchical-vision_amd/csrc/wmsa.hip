@@ -284,16 +284,31 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   auto qld = [&](uint32_t off) { return QNT ? hvk_bld16_nt(r_qkv, off) : hvk_bld16(r_qkv, off); };
   uint4 qf[TPW], kf[TPW], df[TPW], vf[NT];
   int rown[TPW];  // own token rows of the next window, -1 = padding
-  // token rows of window w (recomputed per load, not hoisted into registers that would spill:
-  // a spill reload would wait (vmcnt) for every store left in flight)
+  // token rows of window w, recomputed per load (not hoisted into registers that would spill: a
+  // spill reload would wait (vmcnt) for every store left in flight).  The lane's window-local
+  // (row, column) of tile t sits in byte t of tyx (0xFF: padding), so a row is the window's
+  // scalar origin + ty W + tx, less H W / W where the cyclic shift wraps it (window_token_row's
+  // arithmetic without its per-tile divisions: ~20 VALU per tile before)
+  uint32_t tyx = 0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int tok = 16 * t + li;
+    tyx |= (tok < K::N ? (uint32_t)((tok / WIN) | ((tok % WIN) << 4)) : 0xFFu) << (8 * t);
+  }
   auto token_rows = [&](int w, int (&rt)[NT]) {
     const int b = w / per_img, rem = w % per_img, wh = rem / g.nWw, ww = rem % g.nWw;
-    int lw = li;
-    asm volatile("" : "+v"(lw));
+    const int y0 = wh * WIN + g.shift, x0 = ww * WIN + g.shift;
+    const int base = (b * g.H + y0) * g.W + x0, yl = g.H - y0, xl = g.W - x0, hw = g.H * g.W;
+    uint32_t e4 = tyx;
+    asm volatile("" : "+v"(e4));
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int tok = 16 * t + lw;
-      rt[t] = tok < K::N ? window_token_row(g, b, wh, ww, WIN, tok) : -1;
+      const uint32_t e = (e4 >> (8 * t)) & 0xFFu;
+      const int ty = (int)(e & 15u), tx = (int)(e >> 4);
+      int r = base + ty * g.W + tx;
+      r -= ty >= yl ? hw : 0;
+      r -= tx >= xl ? g.W : 0;
+      rt[t] = e == 0xFFu ? -1 : (int)HVK_BCHECK(r, (long long)g.B * hw);
     }
   };
   auto load_tiles = [&](int w) {

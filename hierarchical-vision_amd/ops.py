@@ -844,9 +844,10 @@ def _ln_out(a, rows):
 
 class LinearLNFn(torch.autograd.Function):
     """(x, xb) = LayerNormResidual(LinearFn(inp, W), abias, x0, ...) with the norm in the GEMM's
-    epilogue (hvk_linear_ln_fwd, C = 96: the stage-0 proj and the patch embedding): one kernel
-    forward instead of two with the same a / x / xb / mean / rstd bits; backward = the LayerNorm
-    backward, then the Linear's (input grad + weight grad, the proj's xshift included)."""
+    epilogue (hvk_linear_ln_fwd; C = 96: the stage-0 proj and the patch embedding on the skinny
+    kernel; C = 192: the stage-1 proj and the stage-0 -> 1 PatchMerging on the 128 x 192 tile): one
+    kernel forward instead of two with the same a / x / xb / mean / rstd bits; backward = the
+    LayerNorm backward, then the Linear's (input grad + weight grad, the proj's xshift included)."""
 
     @staticmethod
     def forward(ctx, inp, weight, xshift, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
@@ -888,8 +889,10 @@ class LinearLNFn(torch.autograd.Function):
 
 
 def linear_ln_supported(M, K, N):
-    """The fused Linear + post-norm (hvk_linear_ln_fwd) is built for this shape and enabled."""
-    return OPTIONS.ln_epilogue and bool(_lib.load().hvk_linear_ln_supported(M, K, N))
+    """The fused Linear + post-norm (hvk_linear_ln_fwd) is built for this shape and enabled
+    (options.ln_epilogue; the C = 192 tile form also options.ln_epilogue_tile)."""
+    return (OPTIONS.ln_epilogue and (N == 96 or OPTIONS.ln_epilogue_tile)
+            and bool(_lib.load().hvk_linear_ln_supported(M, K, N)))
 
 
 def linear_ln(inp, weight, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5, abias=None,
@@ -1102,10 +1105,12 @@ class MlpFn(torch.autograd.Function):
 
 
 class MlpLNFn(torch.autograd.Function):
-    """(x, xb) = LayerNormResidual(fc2(GELU(fc1(inp))), abias = fc2's bias, x0, ...) at the stage-0
-    width as ONE kernel forward (hvk_mlp_ln_fwd: the fused MLP with the block's norm2 in its
-    epilogue, bit-identical to hvk_mlp_fwd + hvk_ln_residual_fwd); backward = the LayerNorm
-    backward, then MlpFn's fused chain (fc2's bias gradient is the norm's dabias)."""
+    """(x, xb) = LayerNormResidual(fc2(GELU(fc1(inp))), abias = fc2's bias, x0, ...).  Stage-0
+    width: ONE kernel forward (hvk_mlp_ln_fwd: the fused MLP with the block's norm2 in its
+    epilogue, bit-identical to hvk_mlp_fwd + hvk_ln_residual_fwd).  Stage-1 width (N2 = 192):
+    fc1 + GELU as MlpFn's kernel, fc2 on the 128 x 192 tile with the norm in its epilogue
+    (hvk_linear_ln_fwd).  Backward = the LayerNorm backward, then MlpFn's chain for the path taken
+    (fc2's bias gradient is the norm's dabias)."""
 
     @staticmethod
     def forward(ctx, inp, w1, b1, w2, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
@@ -1116,17 +1121,23 @@ class MlpLNFn(torch.autograd.Function):
         N2 = w2b.shape[0]
         x2 = xin.reshape(-1, K)
         M = x2.shape[0]
-        h = torch.empty((M, N1), device=x2.device, dtype=torch.bfloat16)
-        y1 = torch.empty_like(h)
         a = torch.empty((*xin.shape[:-1], N2), device=xin.device, dtype=torch.bfloat16)
         x, xb, mean, rstd = _ln_out(a, M)
         gamma, beta = _f32(gamma), _f32(beta)
         abias = _f32(abias) if abias is not None else None
         x0 = _f32(x0) if x0 is not None else None
         sample_scale = _f32(sample_scale) if sample_scale is not None else None
-        call("hvk_mlp_ln_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(w2b), ptr(h), ptr(y1), ptr(a), M, K, N1, N2,
-             ptr(abias), ptr(x0), ptr(gamma), ptr(beta), ptr(sample_scale), rows_per_sample, float(eps), ptr(x),
-             ptr(xb), ptr(mean), ptr(rstd), stream())
+        ln_args = (ptr(abias), ptr(x0), ptr(gamma), ptr(beta), ptr(sample_scale), rows_per_sample, float(eps))
+        ctx.fused = bool(_lib.load().hvk_mlp_ln_supported(M, K, N1, N2))
+        if ctx.fused:
+            h = torch.empty((M, N1), device=x2.device, dtype=torch.bfloat16)
+            y1 = torch.empty_like(h)
+            call("hvk_mlp_ln_fwd", ptr(x2), ptr(w1b), ptr(_f32(b1)), ptr(w2b), ptr(h), ptr(y1), ptr(a), M, K, N1,
+                 N2, *ln_args, ptr(x), ptr(xb), ptr(mean), ptr(rstd), stream())
+        else:
+            h, y1 = gelu_fwd(x2, w1b, b1)
+            call("hvk_linear_ln_fwd", ptr(y1), ptr(w2b), M, N1, N2, *ln_args, ptr(a), ptr(x), ptr(xb), ptr(mean),
+                 ptr(rstd), stream())
         ctx.save_for_backward(xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd)
         ctx.wts = (w1t, w2t)
         ctx.has_x0 = x0 is not None
@@ -1141,7 +1152,8 @@ class MlpLNFn(torch.autograd.Function):
         if r is None:
             return (None,) * 11
         ga, dabias, gx0, dgamma, dbeta = r
-        gin, dw1, db1, dw2 = _mlp_bwd(ga, xin, w1b, w2b, h, y1, ctx.wts, ctx.needs_input_grad[0])
+        bwd = _mlp_bwd if ctx.fused else _mlp_bwd_tiled
+        gin, dw1, db1, dw2 = bwd(ga, xin, w1b, w2b, h, y1, ctx.wts, ctx.needs_input_grad[0])
         return gin, dw1, db1, dw2, dabias, gx0, dgamma, dbeta, None, None, None
 
 
@@ -1167,11 +1179,41 @@ def _mlp_bwd(gy, xb, w1b, w2b, h, y1, wts, want_x):
     return gx, dw1, db1, dw2
 
 
+def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x):
+    """MlpFn's unfused backward chain (fc2's input gradient through GELU' as one kernel, fc1's
+    input gradient, both weight gradients; fc2's bias gradient is the caller's): (gx, dW1, db1,
+    dW2)."""
+    N1, K = w1b.shape
+    N2 = w2b.shape[0]
+    g2 = _bf16(gy).reshape(-1, N2)
+    M = g2.shape[0]
+    dw2 = weight_grad(g2, y1)[0]
+    gh = torch.empty_like(h)
+    w2t = _bf16_t(w2b, wts[1])
+    if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
+                                     _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
+        call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
+    else:
+        call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1, stream())
+    gx = None
+    if want_x:
+        gx = (mm_nt(gh, _bf16_t(w1b, wts[0])) if _native_nt(M, N1, K) else gh @ w1b).reshape(xb.shape)
+    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+    return gx, dw1, db1, dw2
+
+
 def mlp_ln_supported(M, K, N1, N2):
-    """The fused MLP + post-norm (hvk_mlp_ln_fwd, and its fused backward chain) applies."""
+    """MlpLNFn applies: the fused stage-0 MLP + post-norm (hvk_mlp_ln_fwd and its fused backward
+    chain), or fc1 + GELU on MlpFn's kernels with fc2 + post-norm on the tile's LN epilogue."""
+    if not OPTIONS.ln_epilogue:
+        return False
     lib = _lib.load()
-    return (OPTIONS.ln_epilogue and OPTIONS.mlp_fused and bool(lib.hvk_mlp_ln_supported(M, K, N1, N2))
-            and bool(lib.hvk_mlp_bwd_supported(M, N2, N1, K)))
+    if OPTIONS.mlp_fused and lib.hvk_mlp_ln_supported(M, K, N1, N2) and lib.hvk_mlp_bwd_supported(M, N2, N1, K):
+        return True
+    return (N2 != 96 and linear_ln_supported(M, N1, N2) and not _gelu_recompute(M, K, N1, N2)
+            and (((K in _gelu_skinny_k() or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N1))
+                 or _tile_ok(M, K, N1))
+            and (lib.hvk_linear_gelu_bwd_supported(M, N2, N1) or _tile_ok(M, N2, N1)))
 
 
 def mlp_ln(x, w1, b1, w2, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5, abias=None):

@@ -32,6 +32,9 @@ class HostOptions:
     # C = 96 (stage 0): the post-norm LayerNorm + residual in the epilogue of the proj / fc2 /
     # patch-embedding GEMM (hvk_linear_ln_fwd, hvk_mlp_ln_fwd) instead of a separate launch
     ln_epilogue: bool = True
+    # C = 192 (stage 1): the same on the 128 x 192 tile (proj, fc2, the stage-0 -> 1 PatchMerging);
+    # needs ln_epilogue
+    ln_epilogue_tile: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

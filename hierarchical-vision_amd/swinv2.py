@@ -400,6 +400,11 @@ class PatchMerging(nn.Module):
         assert L == H * W, "input feature has wrong size"
         assert H % 2 == 0 and W % 2 == 0, f"x size ({H}*{W}) are not even."
         xm = ops.patch_merge_gather(s.bf16, H, W)
+        if s.bf16.is_cuda and ops.linear_ln_supported(B * L // 4, 4 * C, 2 * C):
+            # 2C = 192 (stage 0 -> 1): the reduction GEMM with its norm in the epilogue
+            x, xb = ops.linear_ln(xm, self.reduction.weight, None, self.norm.weight, self.norm.bias, None, 1,
+                                  self.norm.eps)
+            return ResidualStream(x, xb)
         y = ops.linear(xm, self.reduction.weight)
         x, xb = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1,
                                         self.norm.eps)

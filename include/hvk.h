@@ -186,8 +186,10 @@ int hvk_mlp_fwd(const void* x, const void* w1, const float* b1, const void* w2, 
  * backward reads it) and x = x0 + s[b] (gamma (a + abias - mean) rstd + beta), xb = bf16(x), mean,
  * rstd come out of the same pass, bit-identical to hvk_ln_residual_fwd on that a (same lane layout
  * and arithmetic).  x0 NULL: plain norm; sample_scale NULL: no DropPath; xb_out NULL: not stored.
- * linear: N = 96 with K = 96 (proj) or K = 48 (the patch embedding); mlp: the hvk_mlp_fwd shape with
- * the fc2 output normalised (fc2's bias passed as abias).  ABI 11. */
+ * linear: N = 96 with K = 96 (proj) or K = 48 (the patch embedding) on the skinny kernel, and N = 192
+ * with K % 64 == 0 (SwinV2-T stage 1: proj, fc2, the stage-0 -> 1 PatchMerging) on the 128 x 192 tile
+ * (bit-identical to hvk_gemm_fwd + hvk_ln_residual_fwd); mlp: the hvk_mlp_fwd shape with the fc2
+ * output normalised (fc2's bias passed as abias).  ABI 11. */
 int hvk_linear_ln_supported(int M, int K, int N);
 int hvk_linear_ln_fwd(const void* x, const void* w, int M, int K, int N, const float* abias, const float* x0,
                       const float* gamma, const float* beta, const float* sample_scale, int rows_per_sample,

@@ -1,9 +1,10 @@
-"""The post-norm LayerNorm + residual fused into the producing GEMM's epilogue at C = 96
-(hvk_linear_ln_fwd: the stage-0 proj and the patch embedding; hvk_mlp_ln_fwd: the stage-0 fused
-MLP) against the two launches they replace (the GEMM without its bias, then
-hvk_ln_residual_fwd with that bias as abias): a, x, xb, mean and rstd bit for bit -- the epilogue
-runs ln_fwd_kernel<8, 16>'s lane layout and arithmetic -- and the block / model paths that route
-through them (options.ln_epilogue) equal the unfused ones in outputs and gradients."""
+"""The post-norm LayerNorm + residual fused into the producing GEMM's epilogue (hvk_linear_ln_fwd:
+C = 96 the stage-0 proj and the patch embedding on the skinny kernel, C = 192 the stage-1 proj / fc2
+and the stage-0 -> 1 PatchMerging on the 128 x 192 tile; hvk_mlp_ln_fwd: the stage-0 fused MLP)
+against the two launches they replace (the GEMM without its bias, then hvk_ln_residual_fwd with
+that bias as abias): a, x, xb, mean and rstd bit for bit -- the epilogues run ln_fwd_kernel<8, 16>
+/ <8, 32>'s lane layout and arithmetic -- and the block / model paths that route through them
+(options.ln_epilogue) equal the unfused ones in outputs and gradients."""
 import pytest
 import torch
 
@@ -44,18 +45,22 @@ def _same(a, b, name):
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), name
 
 
-@pytest.mark.parametrize("M,K", [(4099, 96), (50176, 96), (12544 * 2, 48), (1000, 48)])
+@pytest.mark.parametrize("M,K,C", [(4099, 96, 96), (50176, 96, 96), (12544 * 2, 48, 96), (1000, 48, 96),
+                                   (4099, 192, 192), (50176, 768, 192), (1000, 384, 192), (200704, 192, 192)])
 @pytest.mark.parametrize("with_x0,with_dp", [(True, True), (True, False), (False, False)])
-def test_linear_ln_bit_identical(M, K, with_x0, with_dp):
+def test_linear_ln_bit_identical(M, K, C, with_x0, with_dp):
     lib = _lib()
-    C, rps = 96, 49 if M % 49 == 0 else 1
+    rps = 49 if M % 49 == 0 else 1
     assert lib.load().hvk_linear_ln_supported(M, K, C)
     g = torch.Generator(device="cuda").manual_seed(M + K)
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(C, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     gamma, beta, abias, x0, ss = _params(M, C, M + 7, with_x0, with_dp, rps)
     a0 = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
-    lib.call("hvk_linear_fwd", lib.ptr(x), lib.ptr(w), None, lib.ptr(a0), M, K, C, lib.stream())
+    if C == 96:  # the skinny kernel
+        lib.call("hvk_linear_fwd", lib.ptr(x), lib.ptr(w), None, lib.ptr(a0), M, K, C, lib.stream())
+    else:  # the 128 x 192 tile
+        lib.call("hvk_gemm_fwd", lib.ptr(x), lib.ptr(w), None, lib.ptr(a0), M, K, C, lib.stream())
     ref = _ln_ref(a0, abias, x0, gamma, beta, ss, rps, 1e-5)
     a1 = torch.full_like(a0, float("nan"))
     out = [torch.full_like(ref[0], float("nan")), torch.full_like(ref[1], float("nan")),
@@ -108,19 +113,23 @@ def _run_block(blk, x, on, seed):
     return y.detach(), {n: p.grad.detach().clone() for n, p in blk.named_parameters() if p.grad is not None}
 
 
+@pytest.mark.parametrize("C,heads,B", [(96, 3, 4), (192, 6, 42)])
 @pytest.mark.parametrize("shift", [0, 3])
-def test_stage0_block_fused_norms_equal_unfused(shift):
-    """A stage-0 SwinV2 block (C = 96, 3 heads) with the norms fused into proj / the MLP kernel
-    against the unfused launches: output bit-identical, every parameter gradient equal (the
-    backward runs the same kernels on the same saved tensors)."""
+def test_block_fused_norms_equal_unfused(shift, C, heads, B):
+    """A stage-0 (C = 96, 3 heads) / stage-1 (C = 192, 6 heads; B * 784 >= 32 768 tokens so the
+    unfused proj / fc2 run on the same tile kernel) SwinV2 block with the norms fused into proj
+    and the MLP against the unfused launches: output bit-identical, every parameter gradient
+    equal (the backward runs the same kernels on the same saved tensors)."""
     import hvamd.swinv2 as sw
+    from hvamd import ops
     torch.manual_seed(1)
-    blk = sw.SwinTransformerBlock(96, (28, 28), 3, window_size=7, shift_size=shift).cuda().train()
+    blk = sw.SwinTransformerBlock(C, (28, 28), heads, window_size=7, shift_size=shift).cuda().train()
     with torch.no_grad():
         for n in (blk.norm1, blk.norm2):
             n.weight.normal_()
             n.bias.normal_()
-    x = torch.randn(4, 28 * 28, 96, device="cuda")
+    assert ops.linear_ln_supported(B * 784, C, C) and ops.mlp_ln_supported(B * 784, C, 4 * C, C)
+    x = torch.randn(B, 28 * 28, C, device="cuda")
     y0, g0 = _run_block(blk, x, False, 5)
     y1, g1 = _run_block(blk, x, True, 5)
     assert torch.equal(y0.view(torch.int32), y1.view(torch.int32))
@@ -151,3 +160,36 @@ def test_patch_embed_fused_norm_equal_unfused():
     for n in outs[0][2]:
         rel = ((outs[0][2][n] - outs[1][2][n]).norm() / (outs[0][2][n].norm() + 1e-30)).item()
         assert rel < 1e-6, (n, rel)
+
+
+def test_patch_merging_fused_norm_equal_unfused():
+    """The stage-0 -> 1 PatchMerging (2C = 192): the reduction GEMM with its norm in the tile's
+    epilogue against GEMM + LayerNorm launch, bit-identical output and equal gradients."""
+    import hvamd.swinv2 as sw
+    from hvamd import ops
+    torch.manual_seed(3)
+    pm = sw.PatchMerging((56, 56), dim=96).cuda()
+    with torch.no_grad():
+        pm.norm.weight.normal_()
+        pm.norm.bias.normal_()
+    B = 42
+    assert ops.linear_ln_supported(B * 784, 384, 192)
+    x = torch.randn(B, 56 * 56, 96, device="cuda", requires_grad=True)
+    outs = []
+    for on in (False, True):
+        pm.zero_grad(set_to_none=True)
+        x.grad = None
+        with options_override(ln_epilogue=on), torch.autocast("cuda", dtype=torch.bfloat16):
+            s = pm.forward_stream(sw.ResidualStream(x, x.bfloat16()))
+        (s.f32.square().mean() + s.bf16.float().mean()).backward()
+        outs.append((s.f32.detach(), s.bf16.detach(), {n: p.grad.clone() for n, p in pm.named_parameters()}))
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
+    assert torch.equal(outs[0][1].view(torch.int16), outs[1][1].view(torch.int16))
+    for n in outs[0][2]:
+        rel = ((outs[0][2][n] - outs[1][2][n]).norm() / (outs[0][2][n].norm() + 1e-30)).item()
+        assert rel < 1e-6, (n, rel)
+
+
+def options_override(**kw):
+    from hvamd import options
+    return options.override(**kw)
