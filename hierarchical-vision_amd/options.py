@@ -33,8 +33,10 @@ class HostOptions:
     # patch-embedding GEMM (hvk_linear_ln_fwd, hvk_mlp_ln_fwd) instead of a separate launch
     ln_epilogue: bool = True
     # C = 192 (stage 1): the same on the 128 x 192 tile (proj, fc2, the stage-0 -> 1 PatchMerging);
-    # needs ln_epilogue
-    ln_epilogue_tile: bool = True
+    # needs ln_epilogue.  Off: measured -0.85 % end to end (3 interleaved pairs,
+    # profiles/round5/ln_epilogue/ab_tile.txt): the 16 dependent norm passes per tile expose their
+    # shuffle / residual-load latency at the tile kernel's 2 waves per SIMD
+    ln_epilogue_tile: bool = False
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

@@ -107,7 +107,7 @@ def _run_block(blk, x, on, seed):
     blk.zero_grad(set_to_none=True)
     blk._dp = None
     torch.manual_seed(seed)
-    with options.override(ln_epilogue=on), torch.autocast("cuda", dtype=torch.bfloat16):
+    with options.override(ln_epilogue=on, ln_epilogue_tile=on), torch.autocast("cuda", dtype=torch.bfloat16):
         y = blk(x)
     y.float().square().mean().backward()
     return y.detach(), {n: p.grad.detach().clone() for n, p in blk.named_parameters() if p.grad is not None}
@@ -128,7 +128,8 @@ def test_block_fused_norms_equal_unfused(shift, C, heads, B):
         for n in (blk.norm1, blk.norm2):
             n.weight.normal_()
             n.bias.normal_()
-    assert ops.linear_ln_supported(B * 784, C, C) and ops.mlp_ln_supported(B * 784, C, 4 * C, C)
+    with options_override(ln_epilogue_tile=True):
+        assert ops.linear_ln_supported(B * 784, C, C) and ops.mlp_ln_supported(B * 784, C, 4 * C, C)
     x = torch.randn(B, 28 * 28, C, device="cuda")
     y0, g0 = _run_block(blk, x, False, 5)
     y1, g1 = _run_block(blk, x, True, 5)
@@ -173,13 +174,14 @@ def test_patch_merging_fused_norm_equal_unfused():
         pm.norm.weight.normal_()
         pm.norm.bias.normal_()
     B = 42
-    assert ops.linear_ln_supported(B * 784, 384, 192)
+    with options_override(ln_epilogue_tile=True):
+        assert ops.linear_ln_supported(B * 784, 384, 192)
     x = torch.randn(B, 56 * 56, 96, device="cuda", requires_grad=True)
     outs = []
     for on in (False, True):
         pm.zero_grad(set_to_none=True)
         x.grad = None
-        with options_override(ln_epilogue=on), torch.autocast("cuda", dtype=torch.bfloat16):
+        with options_override(ln_epilogue=on, ln_epilogue_tile=on), torch.autocast("cuda", dtype=torch.bfloat16):
             s = pm.forward_stream(sw.ResidualStream(x, x.bfloat16()))
         (s.f32.square().mean() + s.bf16.float().mean()).backward()
         outs.append((s.f32.detach(), s.bf16.detach(), {n: p.grad.clone() for n, p in pm.named_parameters()}))
