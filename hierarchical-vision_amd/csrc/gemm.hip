@@ -132,8 +132,7 @@ __device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t s
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staging reads are back before the next pass's writes
-#pragma unroll
-    for (int m = TPR / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    s = hvk_xor_sum<TPR>(s);
     const float mu = s * invC;
     float ss = 0.f;
 #pragma unroll
@@ -142,8 +141,7 @@ __device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t s
 #pragma unroll
         for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
       }
-#pragma unroll
-    for (int m = TPR / 2; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+    ss = hvk_xor_sum<TPR>(ss);
     const float rs = hvk_ln_rstd(ss, invC, p.eps);
     if (row >= M) continue;
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;

@@ -329,8 +329,7 @@ __device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int
         for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
       }
     }
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    s = hvk_xor_sum<32>(s);
     const float mu = s * invC;
     float ss = 0.f;
 #pragma unroll
@@ -339,8 +338,7 @@ __device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int
 #pragma unroll
         for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
       }
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) ss += __shfl_xor(ss, m);
+    ss = hvk_xor_sum<32>(ss);
     const float rs = hvk_ln_rstd(ss, invC, p.eps);
     if (row >= M) continue;
     const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;

