@@ -64,8 +64,15 @@ __device__ __forceinline__ int perm_row(int p) {
 // 4 (16 i + t)) and runs that kernel's arithmetic on it, so x, xb, mean and rstd are bit-identical
 // to the two-launch path (tests/test_gpu_linear_ln.py).
 // LnEpi (hvk_common.h): the norm's parameters and outputs
+#ifndef HVK_LN96_U  // norm passes (4 rows each) staged and reduced together (A/B build switch: 1, 2)
+#define HVK_LN96_U 2
+#endif
 namespace ln96 {
-constexpr int C = 96, TPR = 16, NG = 2, EPT = 8, STAGE_BYTES = 4 * C * 2;
+// U passes of 4 rows share one staging write / wait / read round and run their row reductions as
+// independent chains (one pass at a time serialised each pass's LDS round trip and shuffles);
+// U = 2 keeps the fused MLP kernel inside one CU's LDS (162 816 of 163 840 B)
+constexpr int U = HVK_LN96_U;
+constexpr int C = 96, TPR = 16, NG = 2, EPT = 8, STAGE_BYTES = U * 4 * C * 2;
 constexpr int PARAM_BYTES = 3 * C * 4;
 // gamma, beta, abias as a [3][96] f32 table in LDS (one copy per workgroup, written before the
 // workgroup's first barrier), read per pass instead of pinning 24 VGPRs per lane
@@ -104,66 +111,77 @@ __device__ __forceinline__ void tile(const LnEpi& p, const Params& q, uint32_t s
   const int t = lane & (TPR - 1), sub = lane / TPR;
   const float invC = 1.f / C;
 #pragma unroll
-  for (int pp = 0; pp < 4; ++pp) {
-    if ((li >> 2) == pp) {
+  for (int p0 = 0; p0 < 4; p0 += U) {
+    // rows 4 p0 .. 4 (p0 + U) - 1 of the tile into the staging buffer (row 4 u + k at u * 768 + k * 192)
+    if ((li >> 2) >= p0 && (li >> 2) < p0 + U) {
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        *reinterpret_cast<__attribute__((address_space(3))) hvk_u32x4*>((__attribute__((address_space(3))) char*)(size_t)(stage + (li & 3) * C * 2 + (32 * j + 8 * g) * 2)) =
+        *reinterpret_cast<__attribute__((address_space(3))) hvk_u32x4*>((__attribute__((address_space(3))) char*)(size_t)(stage + (li - 4 * p0) * C * 2 + (32 * j + 8 * g) * 2)) =
             __builtin_bit_cast(hvk_u32x4, av[j]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int row = row0 + 4 * pp + sub;
-    float v[EPT];
-    float s = 0.f;
+    float v[U][EPT], s[U], mu[U], ss[U], rs[U];
 #pragma unroll
-    for (int i = 0; i < NG; ++i) {
-      if (grp_ok(t, i)) {
+    for (int u = 0; u < U; ++u) {
+      s[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        if (grp_ok(t, i)) {
+          const int c = 4 * (i * TPR + t);
+          const hvk_u32x2 w = *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x2*>(
+              (const __attribute__((address_space(3))) char*)(size_t)(stage + (4 * u + sub) * C * 2 + c * 2));
+          v[u][4 * i] = hvk_lo(w[0]); v[u][4 * i + 1] = hvk_hi(w[0]); v[u][4 * i + 2] = hvk_lo(w[1]); v[u][4 * i + 3] = hvk_hi(w[1]);
+          const float4 ab = param4(q, 2, c);
+          const float abv[4] = {ab.x, ab.y, ab.z, ab.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[u][4 * i + j] += abv[j]; s[u] += v[u][4 * i + j]; }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[u][4 * i + j] = 0.f;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staging reads are back before the next round's writes
+#pragma unroll
+    for (int u = 0; u < U; ++u) mu[u] = hvk_xor_sum<TPR>(s[u]) * invC;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ss[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NG; ++i)
+        if (grp_ok(t, i)) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ss[u] = hvk_ln_sq(ss[u], v[u][4 * i + j] - mu[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) rs[u] = hvk_ln_rstd(hvk_xor_sum<TPR>(ss[u]), invC, p.eps);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int pp = p0 + u;
+      const int row = row0 + 4 * pp + sub;
+      if (row >= M) continue;
+      const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
+      const size_t rb = (size_t)row * C;
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        if (!grp_ok(t, i)) continue;
         const int c = 4 * (i * TPR + t);
-        const hvk_u32x2 u = *reinterpret_cast<const __attribute__((address_space(3))) hvk_u32x2*>(
-            (const __attribute__((address_space(3))) char*)(size_t)(stage + sub * C * 2 + c * 2));
-        v[4 * i] = hvk_lo(u[0]); v[4 * i + 1] = hvk_hi(u[0]); v[4 * i + 2] = hvk_lo(u[1]); v[4 * i + 3] = hvk_hi(u[1]);
-        const float4 ab = param4(q, 2, c);
-        const float abv[4] = {ab.x, ab.y, ab.z, ab.w};
+        float r[4] = {__uint_as_float(x0v[pp][i].x), __uint_as_float(x0v[pp][i].y), __uint_as_float(x0v[pp][i].z),
+                      __uint_as_float(x0v[pp][i].w)};
+        const float4 g4 = param4(q, 0, c), b4 = param4(q, 1, c);
+        const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { v[4 * i + j] += abv[j]; s += v[4 * i + j]; }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
+        for (int j = 0; j < 4; ++j) r[j] = hvk_ln_out(r[j], v[u][4 * i + j], mu[u], rs[u], gm[j], bt[j], sc);
+        const uint4 xr = make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3]));
+        if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
+        else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
+        if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(r[0], r[1]), hvk_pack2(r[2], r[3]));
       }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the staging reads are back before the next pass's writes
-    s = hvk_xor_sum<TPR>(s);
-    const float mu = s * invC;
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < NG; ++i)
-      if (grp_ok(t, i)) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
+      if (t == 0) {
+        p.mean[row] = mu[u];
+        p.rstd[row] = rs[u];
       }
-    ss = hvk_xor_sum<TPR>(ss);
-    const float rs = hvk_ln_rstd(ss, invC, p.eps);
-    if (row >= M) continue;
-    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-    const size_t rb = (size_t)row * C;
-#pragma unroll
-    for (int i = 0; i < NG; ++i) {
-      if (!grp_ok(t, i)) continue;
-      const int c = 4 * (i * TPR + t);
-      float r[4] = {__uint_as_float(x0v[pp][i].x), __uint_as_float(x0v[pp][i].y), __uint_as_float(x0v[pp][i].z),
-                    __uint_as_float(x0v[pp][i].w)};
-      const float4 g4 = param4(q, 0, c), b4 = param4(q, 1, c);
-      const float gm[4] = {g4.x, g4.y, g4.z, g4.w}, bt[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = hvk_ln_out(r[j], v[4 * i + j], mu, rs, gm[j], bt[j], sc);
-      const uint4 xr = make_uint4(__float_as_uint(r[0]), __float_as_uint(r[1]), __float_as_uint(r[2]), __float_as_uint(r[3]));
-      if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
-      else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
-      if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(r[0], r[1]), hvk_pack2(r[2], r[3]));
-    }
-    if (t == 0) {
-      p.mean[row] = mu;
-      p.rstd[row] = rs;
     }
   }
 }

@@ -278,6 +278,9 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
 // of 4 at 4 (32 i + t); layernorm.hip) with its arithmetic (hvk_ln_*), so x, xb, mean and rstd
 // are bit-identical to the two-launch path (tests/test_gpu_linear_ln.py).  A wave takes 2 rows a
 // pass, 16 passes per tile; the next pass's residual rows are loaded under this pass's math.
+#ifndef HVK_LN192_U  // norm passes interleaved per iteration (A/B build switch: 1, 2, 4)
+#define HVK_LN192_U 2
+#endif
 namespace ln192 {
 constexpr int C = 192, PASSES = BM / 8;
 __device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int m0) {
@@ -308,56 +311,78 @@ __device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int
         d[i] = *reinterpret_cast<const float4*>(p.x0 + (size_t)row * C + 4 * (32 * i + t));
     }
   };
-  float4 xn[2];
-  ld_x0(0, xn);
-  for (int pass = 0; pass < PASSES; ++pass) {
-    const float4 xc[2] = {xn[0], xn[1]};
-    if (pass + 1 < PASSES) ld_x0(pass + 1, xn);
-    const int r = 8 * pass + 2 * wave + sub, row = m0 + r;
-    float v[8];
-    float s = 0.f;
+  // U passes (rows r, r + 8, ...) per iteration, their reductions independent chains the compiler
+  // interleaves (one pass at a time left each shuffle's latency exposed at 2 waves per SIMD)
+  constexpr int U = HVK_LN192_U;
+  float4 xn[U][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (i == 0 || ok1) {
+  for (int u = 0; u < U; ++u) ld_x0(u, xn[u]);
+  for (int pp = 0; pp < PASSES; pp += U) {
+    float4 xc[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      xc[u][0] = xn[u][0];
+      xc[u][1] = xn[u][1];
+    }
+    if (pp + U < PASSES)
+#pragma unroll
+      for (int u = 0; u < U; ++u) ld_x0(pp + U + u, xn[u]);
+    float v[U][8], s[U], mu[U], ss[U], rs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = 8 * (pp + u) + 2 * wave + sub;
+      s[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i == 0 || ok1) {
+          const int c = 4 * (32 * i + t);
+          const uint2 w = *reinterpret_cast<const uint2*>(img + stage_off<C>(r, c >> 3) + ((c & 7) << 1));
+          v[u][4 * i] = hvk_lo(w.x); v[u][4 * i + 1] = hvk_hi(w.x); v[u][4 * i + 2] = hvk_lo(w.y); v[u][4 * i + 3] = hvk_hi(w.y);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[u][4 * i + j] += ab[4 * i + j]; s[u] += v[u][4 * i + j]; }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[u][4 * i + j] = 0.f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) mu[u] = hvk_xor_sum<32>(s[u]) * invC;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ss[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        if (i == 0 || ok1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ss[u] = hvk_ln_sq(ss[u], v[u][4 * i + j] - mu[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) rs[u] = hvk_ln_rstd(hvk_xor_sum<32>(ss[u]), invC, p.eps);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = m0 + 8 * (pp + u) + 2 * wave + sub;
+      if (row >= M) continue;
+      const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
+      const size_t rb = (size_t)row * C;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (!(i == 0 || ok1)) continue;
         const int c = 4 * (32 * i + t);
-        const uint2 u = *reinterpret_cast<const uint2*>(img + stage_off<C>(r, c >> 3) + ((c & 7) << 1));
-        v[4 * i] = hvk_lo(u.x); v[4 * i + 1] = hvk_hi(u.x); v[4 * i + 2] = hvk_lo(u.y); v[4 * i + 3] = hvk_hi(u.y);
+        float o[4] = {xc[u][i].x, xc[u][i].y, xc[u][i].z, xc[u][i].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { v[4 * i + j] += ab[4 * i + j]; s += v[4 * i + j]; }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * i + j] = 0.f;
+        for (int j = 0; j < 4; ++j)
+          o[j] = hvk_ln_out(o[j], v[u][4 * i + j], mu[u], rs[u], gm[4 * i + j], bt[4 * i + j], sc);
+        const uint4 xr = make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+        if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
+        else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
+        if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(o[0], o[1]), hvk_pack2(o[2], o[3]));
       }
-    }
-    s = hvk_xor_sum<32>(s);
-    const float mu = s * invC;
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (i == 0 || ok1) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ss = hvk_ln_sq(ss, v[4 * i + j] - mu);
+      if (t == 0) {
+        p.mean[row] = mu[u];
+        p.rstd[row] = rs[u];
       }
-    ss = hvk_xor_sum<32>(ss);
-    const float rs = hvk_ln_rstd(ss, invC, p.eps);
-    if (row >= M) continue;
-    const float sc = p.sscale ? p.sscale[row / p.rows_per_sample] : 1.f;
-    const size_t rb = (size_t)row * C;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (!(i == 0 || ok1)) continue;
-      const int c = 4 * (32 * i + t);
-      float o[4] = {xc[i].x, xc[i].y, xc[i].z, xc[i].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = hvk_ln_out(o[j], v[4 * i + j], mu, rs, gm[4 * i + j], bt[4 * i + j], sc);
-      const uint4 xr = make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
-      if (HVK_NT_SAVED & 2) hvk_st16_nt(p.x + rb + c, xr);  // read again only at the next LayerNorm
-      else *reinterpret_cast<uint4*>(p.x + rb + c) = xr;
-      if (p.xb) *reinterpret_cast<uint2*>(p.xb + rb + c) = make_uint2(hvk_pack2(o[0], o[1]), hvk_pack2(o[2], o[3]));
-    }
-    if (t == 0) {
-      p.mean[row] = mu;
-      p.rstd[row] = rs;
     }
   }
 }

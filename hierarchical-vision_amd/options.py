@@ -33,10 +33,11 @@ class HostOptions:
     # patch-embedding GEMM (hvk_linear_ln_fwd, hvk_mlp_ln_fwd) instead of a separate launch
     ln_epilogue: bool = True
     # C = 192 (stage 1): the same on the 128 x 192 tile (proj, fc2, the stage-0 -> 1 PatchMerging);
-    # needs ln_epilogue.  Off: measured -0.85 % end to end (3 interleaved pairs,
-    # profiles/round5/ln_epilogue/ab_tile.txt): the 16 dependent norm passes per tile expose their
-    # shuffle / residual-load latency at the tile kernel's 2 waves per SIMD
-    ln_epilogue_tile: bool = False
+    # needs ln_epilogue.  First form -0.85 % end to end (its 16 dependent norm passes per tile
+    # exposed their shuffle / residual-load latency at the tile kernel's 2 waves per SIMD); with two
+    # passes interleaved and DPP row sums +0.2 % (3 interleaved pairs on each of two boxes,
+    # profiles/round5/ln_epilogue/ab_tile*.txt)
+    ln_epilogue_tile: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward
