@@ -40,6 +40,7 @@ OptDef g_opts[HVK_OPT_COUNT] = {
     {"dw_tile", 5, 4, 8},
     {"gemm_xr", 0, 0, 2},
     {"gemm_wide", 0, 0, 1},
+    {"wmsa_fwd_hg", 0, 0, 6},
 };
 int find_opt(const char* name) {
   if (!name) return -1;

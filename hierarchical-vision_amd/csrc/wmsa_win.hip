@@ -551,6 +551,16 @@ int launch_win(FwdArgs& a, hipStream_t st) {
 template <int WIN>
 int win_win(FwdArgs& a, hipStream_t st) {
   const int nH = a.g.nH;
+  // option wmsa_fwd_hg forces the heads per workgroup where it divides nH (A/B runs)
+  const int hg = (int)hvk_opt(HVK_OPT_WMSA_FWD_HG);
+  if (hg == 6 && nH % 6 == 0) return launch_win<WIN, 6>(a, st);
+  if (hg == 4 && nH % 4 == 0) return launch_win<WIN, 4>(a, st);
+  if (hg == 3 && nH % 3 == 0) return launch_win<WIN, 3>(a, st);
+  if (hg == 2 && nH % 2 == 0) return launch_win<WIN, 2>(a, st);
+  if (hg == 1) return launch_win<WIN, 1>(a, st);
+  // 6 heads (SwinV2-T stage 1): 2 per workgroup, 58 vs 60.5 us per launch in-step (round 5 sweep,
+  // profiles/round5/wmsa_fwd_hg.txt; 3 stays best at 12 and 24 heads)
+  if (nH == 6) return launch_win<WIN, 2>(a, st);
   // heads per workgroup: 3 where it divides (SwinV2-T: 3 beat 2, 4, 6, 8 at every stage), else 2
   // (SwinV2-B's 4 / 8 / 16 / 32 heads: 0.614 vs 0.595 with 4, one 128-B line per head pair and
   // part, 7 workgroups per CU: profiles/round3/wmsa_fwd_win/stages_b224_hg2.txt)

@@ -321,3 +321,28 @@ def test_bounds_checked_build_reports_no_violation():
         assert "hvk bounds" not in r.stdout + r.stderr, (r.stdout + r.stderr)[-3000:]
         out[name] = [l for l in r.stdout.splitlines() if l.startswith("sum")]
     assert out["bounds"] == out["product"], out
+
+
+@pytest.mark.parametrize("B,H,W,nh,win,shift", [(2, 14, 14, 12, 7, 3), (2, 7, 7, 24, 7, 0), (3, 16, 16, 4, 8, 4)])
+def test_wmsa_forward_head_groups_bit_identical(B, H, W, nh, win, shift):
+    """Option wmsa_fwd_hg (heads per forward workgroup, win form): the per-(window, head) math does
+    not depend on the grouping, so every group size that divides nH gives the default's bits."""
+    import hvamd._lib as lib
+    from hvamd.ops import call, ptr, stream
+    qkv, tab, scale = _inputs(B, H, W, nh, win, 11)
+    lib.load()
+    C = 32 * nh
+    q = qkv.cuda().bfloat16().contiguous()
+    t, s = tab.cuda().contiguous(), scale.cuda().contiguous()
+    outs = {}
+    for hg in (0, 1, 2, 3, 4, 6):
+        if hg and nh % hg:
+            continue
+        with lib.option("wmsa_fwd_hg", hg):
+            out = torch.full((B, H * W, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+            call("hvk_wmsa_fwd", ptr(q), ptr(out), None, ptr(t), ptr(s), B, H, W, C, nh, win, shift, stream())
+            torch.cuda.synchronize()
+            outs[hg] = out
+    assert torch.isfinite(outs[0].float()).all()
+    for hg, o in outs.items():
+        assert torch.equal(o.view(torch.int16), outs[0].view(torch.int16)), hg
