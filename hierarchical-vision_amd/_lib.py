@@ -75,6 +75,13 @@ SIGNATURES = {
     "hvk_mlp_fwd_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p]),
     "hvk_linear_ln_supported": (_i, [_i, _i, _i]),
+    "hvk_merge_gemm_supported": (_i, [_i, _i, _i, _i, _i]),
+    "hvk_merge_gemm_fwd": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "hvk_merge_linear_ln_supported": (_i, [_i, _i, _i, _i, _i]),
+    "hvk_merge_linear_ln_fwd": (_i, [_p, _p, _i, _i, _i, _i, _i, _p, _p, _f, _p, _p, _p, _p, _p, _p]),
+    "hvk_merge_gemm_dgrad": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p]),
+    "hvk_merge_weight_grad_supported": (_i, [_i, _i, _i, _i, _i]),
+    "hvk_merge_weight_grad": (_i, [_p, _p, _p, _i, _i, _i, _i, _i, _p, _sz, _p]),
     "hvk_linear_ln_fwd": (_i, [_p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p, _p, _p, _p]),
     "hvk_mlp_ln_supported": (_i, [_i, _i, _i, _i]),
     "hvk_mlp_ln_fwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p, _p,
@@ -110,7 +117,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 11  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
+ABI_VERSION = 12  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
 
 
 def load():

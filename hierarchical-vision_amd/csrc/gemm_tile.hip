@@ -122,9 +122,11 @@ __device__ __forceinline__ void stage_write(char* smem, const hvk_u32x4 (&v)[MT]
       *reinterpret_cast<hvk_u32x4*>(smem + stage_off<BN>(r0 + 16 * b + li, c0 + 4 * j + gq)) = v[b][j];
 }
 // every 16-B chunk of the 128 x BN image -> Y rows m0 .., columns n0 ..: all LDS reads first,
-// then the stores back to back
-template <int BN, bool NTS, int BM_ = 128, int THREADS = 256>
-__device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restrict__ Y, int M, int N, int m0, int n0) {
+// then the stores back to back.  SC: Y is PatchMerging's token tensor and the image rows are
+// merged rows, each chunk scattered to its source token (hvk_merge_tok / hvk_merge_col)
+template <int BN, bool NTS, int BM_ = 128, int THREADS = 256, bool SC = false>
+__device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restrict__ Y, int M, int N, int m0, int n0,
+                                            const MergeGeo& mg = MergeGeo{}) {
   constexpr int CPR = BN / 8, PER = BM_ * CPR / THREADS;
   static_assert(BM_ * CPR % THREADS == 0, "whole store rounds");
   hvk_u32x4 v[PER];
@@ -137,7 +139,9 @@ __device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restri
   for (int i = 0; i < PER; ++i) {
     const int c = threadIdx.x + THREADS * i, row = c / CPR, cc = c - row * CPR;
     if (m0 + row < M) {
-      hvk_u32x4* dst = reinterpret_cast<hvk_u32x4*>(Y + (size_t)(m0 + row) * N + n0 + 8 * cc);
+      hvk_u32x4* dst = reinterpret_cast<hvk_u32x4*>(
+          SC ? Y + (size_t)hvk_merge_tok(m0 + row, mg) * mg.C + hvk_merge_col(n0 + 8 * cc, mg)
+             : Y + (size_t)(m0 + row) * N + n0 + 8 * cc);
       if (NTS) __builtin_nontemporal_store(v[i], dst);
       else *dst = v[i];
     }
@@ -147,13 +151,15 @@ __device__ __forceinline__ void stage_store(const char* smem, hvk_bf16* __restri
 // EPI 4 (the qkv Linear of a w <= 8 W-MSA block): Y = acc + bias with every q and k head slice
 // (columns < 2N/3) normalised (hvk_head_normalize8, F.normalize of swinv2.py:229) and its
 // 1 / max(||x||, eps) stored to rn [M, 2N/96]; the v columns as EPI 0.
-template <int EPI, int NT, int MT, int HPRE = 0, int SBN = 0, int SBM = 128, int STHREADS = 256>
+template <int EPI, int NT, int MT, int HPRE = 0, int SBN = 0, int SBM = 128, int STHREADS = 256, bool SC = false>
 __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], const float* __restrict__ bias,
                                               hvk_bf16* __restrict__ Y, hvk_bf16* __restrict__ Y2, int M,
                                               int N, int row0, int col0,
                                               const uint4 (*hpre)[NT / 2] = nullptr, float* __restrict__ rn = nullptr,
                                               const float* __restrict__ qscale = nullptr, char* smem = nullptr,
-                                              int m0 = 0, int n0 = 0) {
+                                              int m0 = 0, int n0 = 0, const MergeGeo& mg = MergeGeo{}) {
+  // SC: Y is PatchMerging's token tensor (EPI 0, staged; stage_store)
+  static_assert(!SC || (EPI == 0 && SBN > 0), "the scattered store is the staged EPI 0 form");
   // SBN > 0: outputs staged through the LDS image of a 128 x SBN tile whose origin is (m0, n0)
   // (every wave of the workgroup calls this; the k-loop's LDS reads are all complete)
   // HPRE: h of token tiles 0 .. HPRE-1 was loaded early by the caller (hpre)
@@ -238,7 +244,7 @@ __device__ __forceinline__ void tile_epilogue(const hvk_f32x4 (&acc)[NT][MT], co
     const int r0 = row0 - m0, c0 = (col0 - n0) / 8;
     stage_write<NT, MT, SBN>(smem, pk, r0, c0);
     lds_sync();
-    stage_store<SBN, EPI == 1 && (HVK_NT_SAVED & 1), SBM, STHREADS>(smem, Y, M, N, m0, n0);  // h: read again only by the backward
+    stage_store<SBN, EPI == 1 && (HVK_NT_SAVED & 1), SBM, STHREADS, SC>(smem, Y, M, N, m0, n0, mg);  // h: read again only by the backward
     if constexpr (EPI == 1) {
       lds_sync();  // every thread's image reads are back before the GELU outputs overwrite it
       stage_write<NT, MT, SBN>(smem, pg, r0, c0);
@@ -388,14 +394,17 @@ __device__ __forceinline__ void rows(const char* img, const LnEpi& p, int M, int
 }
 }  // namespace ln192
 
-template <int EPI, bool PIPE, int TN>
+// MG 1: X is PatchMerging's token tensor [B, H W, C], gathered into the merged rows on the DMA
+// (K = 4C); MG 2: Y is, the merged output rows scattered to it (N = 4C; hvk_common.h MergeGeo)
+template <int EPI, bool PIPE, int TN, int MG = 0>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restrict__ X,
                                                         const hvk_bf16* __restrict__ Wt,
                                                         const float* __restrict__ bias,
                                                         hvk_bf16* __restrict__ Y,
                                                         hvk_bf16* __restrict__ Y2, int M, int N,
                                                         int K, int mtiles, float* __restrict__ rn,
-                                                        const float* __restrict__ qscale, LnEpi ln) {
+                                                        const float* __restrict__ qscale, LnEpi ln,
+                                                        MergeGeo mg) {
   using T = TileCfg<TN>;
   constexpr int BN = T::BN, STAGE_BYTES = T::STAGE, TILE_BYTES = T::WTILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -421,7 +430,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     const int row = 8 * (wave + 4 * i) + lr;
     int xr = m0 + row;
     if (xr >= M) xr = M - 1;  // rows past M: any valid row (never stored)
-    xsrc[i] = (size_t)xr * K + 8 * (lc ^ (row & 7));
+    xsrc[i] = MG == 1 ? (size_t)hvk_merge_tok(xr, mg) * mg.C : (size_t)xr * K + 8 * (lc ^ (row & 7));
   }
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
@@ -432,13 +441,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
     if (HVK_GEMM_PROBE == 3) return;
     char* base = smem + buf * STAGE_BYTES;
     const int k0 = kt * BK;
+    // MG 1: a lane's chunk column k0 + 8 (lc ^ lr) is the same in its 4 rows (row & 7 == lr)
+    const int xk = MG == 1 ? hvk_merge_col(k0 + 8 * (lc ^ lr), mg) : k0;
 #pragma unroll
     for (int i = 0; i < TN; ++i)
       __builtin_amdgcn_global_load_lds((gbl_vptr_t)(Wt + wsrc[i] + k0),
                                        (lds_vptr_t)(base + (wave + 4 * i) * 1024), 16, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + xsrc[i] + k0),
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)(X + xsrc[i] + xk),
                                        (lds_vptr_t)(base + TILE_BYTES + (wave + 4 * i) * 1024), 16, 0, 0);
   };
 
@@ -539,9 +550,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
   if (HVK_GEMM_PROBE == 2 && acc[0][0][0] != 1234.5f) return;
   // EPI 5: `a` leaves as EPI 0 (no bias: it is the norm's abias), then the norm of the image
   static_assert(EPI != 5 || (HVK_TILE_STAGED && TN == 6), "EPI 5 runs on the staged 128 x 192 image");
-  tile_epilogue<EPI == 5 ? 0 : EPI, TN, 4, HPB, HVK_TILE_STAGED ? BN : 0>(acc, EPI == 5 ? nullptr : bias, Y, Y2, M, N,
-                                                                      m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn,
-                                                                      qscale, smem, m0, n0);
+  static_assert(MG != 2 || (HVK_TILE_STAGED && EPI == 0), "MG 2 scatters the staged EPI 0 image");
+  tile_epilogue<EPI == 5 ? 0 : EPI, TN, 4, HPB, HVK_TILE_STAGED ? BN : 0, 128, 256, MG == 2>(
+      acc, EPI == 5 ? nullptr : bias, Y, Y2, M, N, m0 + 64 * wm, n0 + 16 * TN * wn, hpre, rn, qscale, smem, m0, n0, mg);
   if constexpr (EPI == 5) ln192::rows(smem, ln, M, m0);
 #if HVK_GEMM_PROBE == 4
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -782,23 +793,23 @@ int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16*
   return -1;
 }
 
-template <int EPI, bool PIPE, int TN>
+template <int EPI, bool PIPE, int TN, int MG = 0>
 int launch_tile_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
                  int M, int N, int K, hipStream_t st, float* rn = nullptr, const float* qscale = nullptr,
-                 const LnEpi& ln = LnEpi{}) {
+                 const LnEpi& ln = LnEpi{}, const MergeGeo& mg = MergeGeo{}) {
   using T = TileCfg<TN>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, PIPE, TN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, PIPE, TN, MG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS);
     attr = true;
   }
   const int mtiles = (M + BM - 1) / BM;
   const int mpad = (mtiles + 7) / 8 * 8;
   const dim3 grid(mpad * (N / T::BN));
-  hvk_timer_shape("gemm_nt", EPI, T::BN, M, N, K, tile_bytes(EPI, M, N, K));
-  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN>), grid, dim3(256),
-                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale, ln);
+  hvk_timer_shape(MG ? "gemm_nt_merge" : "gemm_nt", EPI, T::BN, M, N, K, tile_bytes(EPI, M, N, K));
+  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_nt_kernel<EPI, PIPE, TN, MG>), grid, dim3(256),
+                     T::LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles, rn, qscale, ln, mg);
   HVK_CHECK_LAUNCH("hvk_gemm_tile");
   return HVK_OK;
 }
@@ -839,6 +850,23 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   if (N % TileCfg<4>::BN == 0 && !wide)
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st);
   return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st);
+  }
+}
+
+// PatchMerging's reduction GEMM with the 2x2 gather on its X operand (MG 1: EPI 0, or EPI 5 with
+// the norm) or its input gradient with the scatter in its store (MG 2): the tile launch_tile<0>
+// picks for the same shape with default options, so the bits equal gather + GEMM / GEMM + scatter
+template <int EPI, int MG>
+int launch_merge(const hvk_bf16* X, const hvk_bf16* W, hvk_bf16* Y, int M, int N, int K, const MergeGeo& mg,
+                 hipStream_t st, const LnEpi& ln = LnEpi{}) {
+  if constexpr (EPI == 5) {
+    return launch_tile_<5, true, 6, MG>(X, W, nullptr, Y, nullptr, M, N, K, st, nullptr, nullptr, ln, mg);
+  } else {
+    const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
+    const bool wide = N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1152));
+    if (N % TileCfg<4>::BN == 0 && !wide)
+      return launch_tile_<EPI, true, 4, MG>(X, W, nullptr, Y, nullptr, M, N, K, st, nullptr, nullptr, ln, mg);
+    return launch_tile_<EPI, true, 6, MG>(X, W, nullptr, Y, nullptr, M, N, K, st, nullptr, nullptr, ln, mg);
   }
 }
 
@@ -901,6 +929,64 @@ int hvk_gemm_qkv_fwd(const void* x, const void* w, const float* bias, void* y, f
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_gemm_qkv_fwd: M=%d K=%d N=%d (N = 3C, 32 | C)", M, K, N);
   return launch_tile<4>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), bias,
                         static_cast<hvk_bf16*>(y), nullptr, M, N, K, static_cast<hipStream_t>(stream), rn, qscale);
+}
+
+// ---- PatchMerging (swinv2.py:484-494): gather / scatter folded into the reduction GEMM ----------
+static bool merge_geo(int B, int H, int W, int C, int& M, MergeGeo& g) {
+  if (B <= 0 || H <= 0 || W <= 0 || H % 2 || W % 2 || C <= 0 || C % 8) return false;
+  const long long m = (long long)B * (H / 2) * (W / 2);
+  if (m >= (1ll << 21) || (long long)B * H * W * C >= (1ll << 31)) return false;  // hvk_merge_tok exactness
+  M = (int)m;
+  g.W = W;
+  g.C = C;
+  g.inv_wo = 1.0f / (float)(W / 2);
+  return true;
+}
+
+int hvk_merge_gemm_supported(int B, int H, int W, int C, int N) {
+  int M;
+  MergeGeo g;
+  return merge_geo(B, H, W, C, M, g) && hvk_gemm_supported(M, 4 * C, N) && hvk_gemm_supported(M, N, 4 * C);
+}
+
+int hvk_merge_gemm_fwd(const void* x, const void* w, void* y, int B, int H, int W, int C, int N, void* stream) {
+  if (!x || !w || !y) return hvk_set_error(HVK_EINVAL, "hvk_merge_gemm_fwd: null pointer");
+  int M;
+  MergeGeo g;
+  if (!merge_geo(B, H, W, C, M, g) || !hvk_merge_gemm_supported(B, H, W, C, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_merge_gemm_fwd: B=%d H=%d W=%d C=%d N=%d", B, H, W, C, N);
+  return launch_merge<0, 1>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w), static_cast<hvk_bf16*>(y),
+                            M, N, 4 * C, g, static_cast<hipStream_t>(stream));
+}
+
+int hvk_merge_linear_ln_supported(int B, int H, int W, int C, int N) {
+  int M;
+  MergeGeo g;
+  return merge_geo(B, H, W, C, M, g) && hvk_merge_gemm_supported(B, H, W, C, N) && hvk_tile_ln::supported(M, N, 4 * C);
+}
+
+int hvk_merge_linear_ln_fwd(const void* x, const void* w, int B, int H, int W, int C, int N, const float* gamma,
+                            const float* beta, float eps, void* a_out, float* x_out, void* xb_out, float* mean,
+                            float* rstd, void* stream) {
+  if (!x || !w || !a_out || !gamma || !beta || !x_out || !mean || !rstd)
+    return hvk_set_error(HVK_EINVAL, "hvk_merge_linear_ln_fwd: null pointer");
+  int M;
+  MergeGeo g;
+  if (!merge_geo(B, H, W, C, M, g) || !hvk_merge_linear_ln_supported(B, H, W, C, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_merge_linear_ln_fwd: B=%d H=%d W=%d C=%d N=%d", B, H, W, C, N);
+  const LnEpi ln{nullptr, nullptr, gamma, beta, nullptr, 1, eps, x_out, static_cast<hvk_bf16*>(xb_out), mean, rstd};
+  return launch_merge<5, 1>(static_cast<const hvk_bf16*>(x), static_cast<const hvk_bf16*>(w),
+                            static_cast<hvk_bf16*>(a_out), M, N, 4 * C, g, static_cast<hipStream_t>(stream), ln);
+}
+
+int hvk_merge_gemm_dgrad(const void* gy, const void* wt, void* gx, int B, int H, int W, int C, int N, void* stream) {
+  if (!gy || !wt || !gx) return hvk_set_error(HVK_EINVAL, "hvk_merge_gemm_dgrad: null pointer");
+  int M;
+  MergeGeo g;
+  if (!merge_geo(B, H, W, C, M, g) || !hvk_merge_gemm_supported(B, H, W, C, N))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_merge_gemm_dgrad: B=%d H=%d W=%d C=%d N=%d", B, H, W, C, N);
+  return launch_merge<0, 2>(static_cast<const hvk_bf16*>(gy), static_cast<const hvk_bf16*>(wt),
+                            static_cast<hvk_bf16*>(gx), M, 4 * C, N, g, static_cast<hipStream_t>(stream));
 }
 
 int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, void* y, int M, int K,

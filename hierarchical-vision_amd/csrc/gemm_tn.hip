@@ -85,12 +85,14 @@ __device__ __forceinline__ void wait_stages(int r) {
   }
 }
 
-template <int FK, int FN, int WK, int WN, bool DB, bool GX = false>
+// MG: X is PatchMerging's token tensor [B, H W, C] (K = 4C), its merged rows gathered on the DMA
+// (hvk_common.h MergeGeo): the reduction Linear's weight gradient without the materialised gather
+template <int FK, int FN, int WK, int WN, bool DB, bool GX = false, bool MG = false>
 __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN <= 192) ? 2 : 1) void dw_kernel(const hvk_bf16* __restrict__ G,
                                                            const hvk_bf16* __restrict__ X,
                                                            float* __restrict__ P, int N, int K,
                                                            int ntk, int ntiles, int nslices,
-                                                           int nchunk, long pstride) {
+                                                           int nchunk, long pstride, MergeGeo mg) {
   using C = TnCfg<FK, FN, WK, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // XCD-aware decode: work items (chunk-major: item = c * ntiles + tile) are dealt to the 8
@@ -109,14 +111,18 @@ __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN 
   // DMA: LDS chunk ci = THREADS i + tid of a stage (lane-linear) <- global 16 B of
   // (operand, token row 4 rb + q, column 16 cb + 8 hf); pad subtiles / tail chunks re-read
   // the operand's first row of the stage and land in LDS nobody reads
+  // MG: an x chunk's address is rebuilt per stage from its merged row mrow (-1: a g chunk) and its
+  // column's offset mcol
   const char* src[C::D];
   uint32_t inc[C::D];
+  int mrow[MG ? C::D : 1], mcol[MG ? C::D : 1];
 #pragma unroll
   for (int i = 0; i < C::D; ++i) {
     const int ci = i * C::THREADS + tid;
     const hvk_bf16* base = G + (size_t)sb * TOK * N + n0;
     size_t off = 0;
     uint32_t step = 2u * TOK * N;
+    if (MG) mrow[i] = -1, mcol[i] = 0;
     if (ci < C::REGG / 16) {
       const int rb = ci / (C::RBSG / 16), w = ci % (C::RBSG / 16);
       if (w < 8 * C::NCBG) off = (size_t)(4 * rb + ((w & 7) >> 1)) * N + 16 * (w >> 3) + 8 * (w & 1);
@@ -125,7 +131,12 @@ __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN 
       const int rb = lc / (C::RBSX / 16), w = lc % (C::RBSX / 16);
       base = X + (size_t)sb * TOK * K + k0;
       step = 2u * TOK * K;
-      if (w < 8 * C::NCBX) off = (size_t)(4 * rb + ((w & 7) >> 1)) * K + 16 * (w >> 3) + 8 * (w & 1);
+      const bool real = w < 8 * C::NCBX;
+      if (real) off = (size_t)(4 * rb + ((w & 7) >> 1)) * K + 16 * (w >> 3) + 8 * (w & 1);
+      if (MG) {
+        mrow[i] = sb * TOK + (real ? 4 * rb + ((w & 7) >> 1) : 0);
+        mcol[i] = hvk_merge_col(k0 + (real ? 16 * (w >> 3) + 8 * (w & 1) : 0), mg);
+      }
     }
     src[i] = reinterpret_cast<const char*>(base + off);
     inc[i] = step;
@@ -134,8 +145,14 @@ __global__ __launch_bounds__(64 * WK * WN, (16 * FK * WK == 128 && 16 * FN * WN 
     char* b = smem + buf * C::STAGE + wave * 1024;
 #pragma unroll
     for (int i = 0; i < C::D; ++i) {
-      __builtin_amdgcn_global_load_lds((gbl_vptr_t)src[i], (lds_vptr_t)(b + i * C::THREADS * 16), 16,
-                                       0, 0);
+      const char* p = src[i];
+      if constexpr (MG) {
+        if (mrow[i] >= 0) {
+          p = reinterpret_cast<const char*>(X + (size_t)hvk_merge_tok(mrow[i], mg) * mg.C + mcol[i]);
+          mrow[i] += TOK;
+        }
+      }
+      __builtin_amdgcn_global_load_lds((gbl_vptr_t)p, (lds_vptr_t)(b + i * C::THREADS * 16), 16, 0, 0);
       src[i] += inc[i];
     }
   };
@@ -307,17 +324,17 @@ bool plan(int M, int N, int K, Plan& p) {
   return true;
 }
 
-template <int FK, int FN, int WK, int WN, bool GX = false>
+template <int FK, int FN, int WK, int WN, bool GX = false, bool MG = false>
 int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, int K, const Plan& p,
-           hipStream_t st) {
+           hipStream_t st, const MergeGeo& mg = MergeGeo{}) {
   using C = TnCfg<FK, FN, WK, WN>;
   static_assert(C::TK > 0 && C::TN > 0, "tile");
   if (C::TK != p.tk || C::TN != p.tn) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad: plan/tile mismatch");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, true, GX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, true, GX, MG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, false, GX>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dw_kernel<FK, FN, WK, WN, false, GX, MG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
@@ -325,15 +342,15 @@ int launch(const hvk_bf16* g, const hvk_bf16* x, float* P, bool with_db, int N, 
   const double flops = 2.0 * p.nslices * TOK * N * K;  // g^T x (the fused db adds 2 M N)
   {  // algorithmic bytes: g and x read once, dW (+ db) written once in f32 (partial slabs excluded)
     const double M = (double)p.nslices * TOK;
-    hvk_timer_shape(GX ? "dw_gelu_x" : "dw", with_db ? 1 : 0, C::TN, M, N, K,
+    hvk_timer_shape(GX ? "dw_gelu_x" : MG ? "dw_merge" : "dw", with_db ? 1 : 0, C::TN, M, N, K,
                     2.0 * M * (N + K) + 4.0 * N * K + (with_db ? 4.0 * N : 0.0));
   }
   if (with_db)
-    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, true, GX>), grid, dim3(C::THREADS),
-                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, true, GX, MG>), grid, dim3(C::THREADS),
+                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride, mg);
   else
-    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, false, GX>), grid, dim3(C::THREADS),
-                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride);
+    HVK_LAUNCH_TIMED_W(HVK_TIMER_WGRAD, flops, (dw_kernel<FK, FN, WK, WN, false, GX, MG>), grid, dim3(C::THREADS),
+                       C::LDS, st, g, x, P, N, K, p.ntk, p.ntiles, p.nslices, p.nchunk, p.pstride, mg);
   HVK_CHECK_LAUNCH("hvk_weight_grad");
   return HVK_OK;
 }
@@ -354,7 +371,8 @@ size_t hvk_weight_grad_workspace(int M, int N, int K) {
 }
 
 static int weight_grad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, void* ws,
-                       size_t ws_bytes, void* stream, bool gx, const float* xshift = nullptr) {
+                       size_t ws_bytes, void* stream, bool gx, const float* xshift = nullptr,
+                       const MergeGeo* mg = nullptr) {
   if (!g || !x || !dw || !ws) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad: null pointer");
   Plan p;
   if (!plan(M, N, K, p))
@@ -369,6 +387,15 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
   int rc;
   if (gx && p.var != V_96x384)
     return hvk_set_error(HVK_EUNSUPPORTED, "hvk_weight_grad_gelu_x: M=%d N=%d K=%d", M, N, K);
+  if (mg) {  // PatchMerging's reduction: the tile variants of its shapes (merge_plan_ok)
+    switch (p.var) {
+      case V_T4: rc = launch<6, 6, 2, 2, false, true>(gb, xb, P, wd, N, K, p, st, *mg); break;
+      case V_T8A: rc = launch<6, 3, 2, 4, false, true>(gb, xb, P, wd, N, K, p, st, *mg); break;
+      case V_B256: rc = launch<4, 4, 2, 4, false, true>(gb, xb, P, wd, N, K, p, st, *mg); break;
+      case V_B128: rc = launch<4, 2, 2, 4, false, true>(gb, xb, P, wd, N, K, p, st, *mg); break;
+      default: return hvk_set_error(HVK_EUNSUPPORTED, "hvk_merge_weight_grad: tile variant %d", p.var);
+    }
+  } else
   switch (gx ? -1 : p.var) {
     case -1: rc = launch<12, 3, 2, 2, true>(gb, xb, P, wd, N, K, p, st); break;
     case V_288x96: rc = launch<3, 9, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
@@ -411,6 +438,36 @@ int hvk_weight_grad_shift(const void* g, const void* x, const float* xshift, flo
                           int K, void* ws, size_t ws_bytes, void* stream) {
   if (!xshift) return hvk_set_error(HVK_EINVAL, "hvk_weight_grad_shift: null xshift");
   return weight_grad(g, x, dw, db, M, N, K, ws, ws_bytes, stream, false, xshift);
+}
+
+static bool merge_plan_ok(int B, int H, int W, int C, int N, int& M, MergeGeo& g) {
+  if (B <= 0 || H <= 0 || W <= 0 || H % 2 || W % 2 || C <= 0 || C % 8) return false;
+  const long long m = (long long)B * (H / 2) * (W / 2);
+  if (m >= (1ll << 21) || (long long)B * H * W * C >= (1ll << 31)) return false;  // hvk_merge_tok exactness
+  M = (int)m;
+  g.W = W;
+  g.C = C;
+  g.inv_wo = 1.0f / (float)(W / 2);
+  Plan p;
+  if (!plan(M, N, 4 * C, p)) return false;
+  return p.var == V_T4 || p.var == V_T8A || p.var == V_B256 || p.var == V_B128;
+}
+
+int hvk_merge_weight_grad_supported(int B, int H, int W, int C, int N) {
+  int M;
+  MergeGeo g;
+  return merge_plan_ok(B, H, W, C, N, M, g) ? 1 : 0;
+}
+
+// dW [N, 4C] of PatchMerging's reduction = gy [M, N]^T gather(x) with x [B, H W, C] the token rows
+// (no bias); workspace hvk_weight_grad_workspace(M, N, 4C), M = B H W / 4
+int hvk_merge_weight_grad(const void* gy, const void* x, float* dw, int B, int H, int W, int C, int N, void* ws,
+                          size_t ws_bytes, void* stream) {
+  int M;
+  MergeGeo g;
+  if (!merge_plan_ok(B, H, W, C, N, M, g))
+    return hvk_set_error(HVK_EUNSUPPORTED, "hvk_merge_weight_grad: B=%d H=%d W=%d C=%d N=%d", B, H, W, C, N);
+  return weight_grad(gy, x, dw, nullptr, M, N, 4 * C, ws, ws_bytes, stream, false, nullptr, &g);
 }
 
 int hvk_weight_grad_gelu_x_supported(int M, int N, int K) {

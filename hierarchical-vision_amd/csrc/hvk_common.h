@@ -145,6 +145,31 @@ struct LnEpi {
   float* rstd;          // [M]
 };
 
+// ---- PatchMerging's 2x2 gather as an operand address map (swinv2.py:484-491) ---------------
+// The reduction GEMM of PatchMerging reads its [B, H/2 * W/2, 4C] operand straight from the
+// token rows [B, H * W, C] (gemm_tile.hip MG 1, gemm_tn.hip MG), and its input gradient is
+// written straight back to them (MG 2): merged row r = (b, i, j), 4C-column k of segment
+// s = k / C (x0 .. x3 = [0::2, 0::2], [1::2, 0::2], [0::2, 1::2], [1::2, 1::2]) is source token
+// (b, 2i + (s & 1), 2j + (s >> 1)), channel k - s C.  Source token of (r, s = 0):
+// (b H + 2i) W + 2j = 2r + W floor(r / (W/2)); the quotient by a float reciprocal, exact while
+// r < 2^21 (|error| <= r / Wo * 2^-23 < 1 / (4 Wo), the distance of (r + 1/2) / Wo to an integer
+// is >= 1 / (2 Wo)); hvk_merge_*_supported bound M.  C % 8 == 0: a 16-B chunk never straddles
+// two segments.
+struct MergeGeo {
+  int W = 0;           // source width (tokens per image row)
+  int C = 0;           // source channels
+  float inv_wo = 0.f;  // 1 / (W / 2)
+};
+__device__ __forceinline__ int hvk_merge_tok(int r, const MergeGeo& g) {
+  const int q = (int)(((float)r + 0.5f) * g.inv_wo);
+  return 2 * r + g.W * q;
+}
+// element offset of 4C-column k of a merged row from its segment-0 token row
+__device__ __forceinline__ int hvk_merge_col(int k, const MergeGeo& g) {
+  const int s = (k >= g.C) + (k >= 2 * g.C) + (k >= 3 * g.C);
+  return ((s & 1) * g.W + (s >> 1)) * g.C + (k - s * g.C);
+}
+
 // ---- post-norm LayerNorm arithmetic, pinned op by op ---------------------------------------
 // ln_fwd_kernel (layernorm.hip) and the GEMM epilogues that reproduce it bit for bit (gemm.hip,
 // ln96) share these: left to the contraction pass, the SLP vectoriser turned `ss += d * d` into

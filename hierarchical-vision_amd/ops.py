@@ -1299,6 +1299,113 @@ def patch_merge_gather(x, H, W):
     return PatchMergeGather.apply(x, H, W)
 
 
+def merge_linear_supported(B, H, W, C, N):
+    """PatchMerging's gather folded into its reduction GEMM both ways (hvk_merge_*; option
+    merge_gemm) for x [B, H*W, C] and the Linear 4C -> N."""
+    if not OPTIONS.merge_gemm:
+        return False
+    lib = _lib.load()
+    return bool(lib.hvk_merge_gemm_supported(B, H, W, C, N) and lib.hvk_merge_weight_grad_supported(B, H, W, C, N))
+
+
+def merge_linear_ln_supported(B, H, W, C, N):
+    """... and with PatchMerging's norm in the GEMM epilogue (N = 192; options ln_epilogue,
+    ln_epilogue_tile)."""
+    return (merge_linear_supported(B, H, W, C, N) and OPTIONS.ln_epilogue and OPTIONS.ln_epilogue_tile
+            and bool(_lib.load().hvk_merge_linear_ln_supported(B, H, W, C, N)))
+
+
+def _merge_linear_bwd(ctx, xb, wb, ga):
+    """Input gradient (scattered to the token rows) and weight gradient (gathering on its DMA) of
+    PatchMerging's reduction Linear for the output gradient ga [M, N] bf16."""
+    B, H, W, C, N = ctx.geo
+    ga = _bf16(ga).contiguous()
+    gx = dw = None
+    if ctx.needs_input_grad[0]:
+        gx = torch.empty((B, H * W, C), device=ga.device, dtype=torch.bfloat16)
+        call("hvk_merge_gemm_dgrad", ptr(ga), ptr(_bf16_t(wb, ctx.wt)), ptr(gx), B, H, W, C, N, stream())
+    if ctx.needs_input_grad[1]:
+        lib = _lib.load()
+        M = B * H * W // 4
+        nb = lib.hvk_weight_grad_workspace(M, N, 4 * C)
+        ws = torch.empty(nb // 4, device=ga.device, dtype=torch.float32)
+        dw = torch.empty((N, 4 * C), device=ga.device, dtype=torch.float32)
+        call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
+    return gx, dw
+
+
+class MergeLinearFn(torch.autograd.Function):
+    """PatchMerging's strided gather + reduction Linear (swinv2.py:484-494) as one GEMM each way:
+    forward hvk_merge_gemm_fwd (the gather on the operand loads), backward hvk_merge_gemm_dgrad
+    (the input gradient scattered by the GEMM's store) and hvk_merge_weight_grad; the same bits
+    as patch_merge_gather + linear, without the [T/4, 4C] tensor."""
+
+    @staticmethod
+    def forward(ctx, x, weight, H, W):
+        xb = _bf16(x).contiguous()
+        wb, wt = _bf16_weight(weight)
+        B, L, C = xb.shape
+        N = wb.shape[0]
+        y = torch.empty((B, L // 4, N), device=xb.device, dtype=torch.bfloat16)
+        call("hvk_merge_gemm_fwd", ptr(xb), ptr(wb), ptr(y), B, H, W, C, N, stream())
+        ctx.save_for_backward(xb, wb)
+        ctx.wt = wt
+        ctx.geo = (B, H, W, C, N)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        gx, dw = _merge_linear_bwd(ctx, xb, wb, gy.reshape(-1, ctx.geo[4]))
+        return gx, dw, None, None
+
+
+class MergeLinearLNFn(torch.autograd.Function):
+    """MergeLinearFn with PatchMerging's norm in the GEMM epilogue (hvk_merge_linear_ln_fwd, N =
+    192: the stage-0 -> 1 merge): (x, xb) as linear_ln(patch_merge_gather(x), ...) bit for bit;
+    backward = the norm's, then MergeLinearFn's."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, eps, H, W):
+        xb = _bf16(x).contiguous()
+        wb, wt = _bf16_weight(weight)
+        B, L, C = xb.shape
+        N = wb.shape[0]
+        M = B * L // 4
+        a = torch.empty((B, L // 4, N), device=xb.device, dtype=torch.bfloat16)
+        xo, xob, mean, rstd = _ln_out(a, M)
+        gamma, beta = _f32(gamma), _f32(beta)
+        call("hvk_merge_linear_ln_fwd", ptr(xb), ptr(wb), B, H, W, C, N, ptr(gamma), ptr(beta), float(eps), ptr(a),
+             ptr(xo), ptr(xob), ptr(mean), ptr(rstd), stream())
+        ctx.save_for_backward(xb, wb, a, gamma, mean, rstd)
+        ctx.wt = wt
+        ctx.geo = (B, H, W, C, N)
+        ctx.set_materialize_grads(False)
+        return xo, xob
+
+    @staticmethod
+    def backward(ctx, gx, gxb):
+        xb, wb, a, gamma, mean, rstd = ctx.saved_tensors
+        r = _ln_residual_bwd(a, None, gamma, None, mean, rstd, 1, False, gx, gxb)
+        if r is None:
+            return (None,) * 7
+        ga, _, _, dgamma, dbeta = r
+        gin, dw = _merge_linear_bwd(ctx, xb, wb, ga.reshape(-1, ctx.geo[4]))
+        return gin, dw, dgamma, dbeta, None, None, None
+
+
+def merge_linear(x, weight, H, W):
+    """F.linear(patch_merge_gather(x, H, W), weight) as one GEMM each way (callers check
+    merge_linear_supported)."""
+    return MergeLinearFn.apply(x, weight, H, W)
+
+
+def merge_linear_ln(x, weight, gamma, beta, eps, H, W):
+    """linear_ln(patch_merge_gather(x, H, W), weight, None, gamma, beta, eps=eps) with the gather
+    in the GEMM (callers check merge_linear_ln_supported)."""
+    return MergeLinearLNFn.apply(x, weight, gamma, beta, eps, H, W)
+
+
 # --------------------------------------------------------------------------- losses
 class MultitaskCE(torch.autograd.Function):
     """sum_h coeff[h] * mean_b CE(logits[:, off[h]:off[h+1]], target_h)."""

@@ -38,6 +38,10 @@ class HostOptions:
     # passes interleaved and DPP row sums +0.2 % (3 interleaved pairs on each of two boxes,
     # profiles/round5/ln_epilogue/ab_tile*.txt)
     ln_epilogue_tile: bool = True
+    # PatchMerging's 2x2 gather folded into its reduction GEMM (operand loads), the input
+    # gradient scattered by the dgrad GEMM's store, the weight gradient gathering on its DMA:
+    # no [T/4, 4C] tensor either way (hvk_merge_*, bit-identical)
+    merge_gemm: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

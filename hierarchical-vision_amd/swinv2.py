@@ -14,7 +14,8 @@ block is re-planned around the hardware:
   that addresses windows by index math.  torch.roll / window_partition /
   window_reverse (swinv2.py:69-102, 399-429) never materialise.
 * Post-norm + DropPath + residual add is one kernel (``ops.layer_norm_residual``).
-* PatchMerging's strided 2x2 gather is one kernel (``ops.patch_merge_gather``).
+* PatchMerging's strided 2x2 gather rides in its reduction GEMM's operand loads both ways
+  (``ops.merge_linear``; ``ops.patch_merge_gather`` + ``ops.linear`` where not built).
 * Dense contractions (qkv, proj, fc1, fc2, reduction, patch embedding) run on
   libhvk's MFMA GEMMs in bf16 under autocast (``ops.linear``: the skinny
   weight-stationary kernel at the SwinV2-T stage 0-1 widths, the tiled kernel
@@ -399,6 +400,15 @@ class PatchMerging(nn.Module):
         B, L, C = s.bf16.shape
         assert L == H * W, "input feature has wrong size"
         assert H % 2 == 0 and W % 2 == 0, f"x size ({H}*{W}) are not even."
+        if s.bf16.is_cuda and ops.merge_linear_supported(B, H, W, C, 2 * C):
+            # the gather folded into the reduction GEMM both ways (no [T/4, 4C] tensor)
+            if ops.merge_linear_ln_supported(B, H, W, C, 2 * C):
+                x, xb = ops.merge_linear_ln(s.bf16, self.reduction.weight, self.norm.weight, self.norm.bias,
+                                            self.norm.eps, H, W)
+                return ResidualStream(x, xb)
+            y = ops.merge_linear(s.bf16, self.reduction.weight, H, W)
+            x, xb = ops.layer_norm_residual(y, None, self.norm.weight, self.norm.bias, None, 1, self.norm.eps)
+            return ResidualStream(x, xb)
         xm = ops.patch_merge_gather(s.bf16, H, W)
         if s.bf16.is_cuda and ops.linear_ln_supported(B * L // 4, 4 * C, 2 * C):
             # 2C = 192 (stage 0 -> 1): the reduction GEMM with its norm in the epilogue

@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 /* the C ABI this header describes; hvk_abi_version() returns it (bindings check it at load) */
-#define HVK_ABI_VERSION 11
+#define HVK_ABI_VERSION 12
 
 #define HVK_OK 0
 #define HVK_EINVAL 1
@@ -417,6 +417,33 @@ int hvk_normalize_u8(const uint8_t* x, float* out, const float* mean, const floa
                      void* stream);
 int hvk_patch_merge_scatter(const void* gout, void* gx, int B, int H, int W, int C,
                             void* stream);
+
+/* ---- PatchMerging as one strided-gather + Linear (swinv2.py:484-494), ABI 12 -------------
+ * The reduction Linear (4C -> N, no bias) with the 2x2 gather above folded into its operand
+ * loads, so the [B, H*W/4, 4C] tensor is never written: x bf16 [B, H*W, C] (the token rows),
+ * w bf16 [N, 4C], M = B*H*W/4 merged rows.  Results are bit-identical to
+ * hvk_patch_merge_gather + hvk_gemm_fwd (and + hvk_linear_ln_fwd, + hvk_gemm_fwd on the input
+ * gradient + hvk_patch_merge_scatter, + hvk_weight_grad) with default options.
+ *   hvk_merge_gemm_fwd:      y bf16 [M, N] = gather(x) w^T
+ *   hvk_merge_linear_ln_fwd: the same with PatchMerging's norm in the epilogue (N = 192):
+ *                            a = gather(x) w^T, x_out / xb_out / mean / rstd as hvk_linear_ln_fwd
+ *                            with no abias, x0 or sample scale
+ *   hvk_merge_gemm_dgrad:    gx bf16 [B, H*W, C] = scatter(gy wt^T), gy bf16 [M, N], wt = w^T
+ *                            bf16 [4C, N] (every element of gx written once)
+ *   hvk_merge_weight_grad:   dw f32 [N, 4C] = gy^T gather(x); workspace
+ *                            hvk_weight_grad_workspace(M, N, 4C)
+ * _supported: H, W even, C % 8 == 0, M < 2^21, and the tiled GEMM / weight-gradient plans of
+ * the shape (K = 4C a multiple of 64, N of 128 or 192). */
+int hvk_merge_gemm_supported(int B, int H, int W, int C, int N);
+int hvk_merge_gemm_fwd(const void* x, const void* w, void* y, int B, int H, int W, int C, int N, void* stream);
+int hvk_merge_linear_ln_supported(int B, int H, int W, int C, int N);
+int hvk_merge_linear_ln_fwd(const void* x, const void* w, int B, int H, int W, int C, int N, const float* gamma,
+                            const float* beta, float eps, void* a_out, float* x_out, void* xb_out, float* mean,
+                            float* rstd, void* stream);
+int hvk_merge_gemm_dgrad(const void* gy, const void* wt, void* gx, int B, int H, int W, int C, int N, void* stream);
+int hvk_merge_weight_grad_supported(int B, int H, int W, int C, int N);
+int hvk_merge_weight_grad(const void* gy, const void* x, float* dw, int B, int H, int W, int C, int N, void* ws,
+                          size_t ws_bytes, void* stream);
 
 /* ---- Multitask / flat cross-entropy (hierarchy.py:65-94; models.py:112) -----------
  * logits: f32 [B, ld]; head h occupies columns [head_off[h], head_off[h+1]).

@@ -181,7 +181,8 @@ def test_patch_merging_fused_norm_equal_unfused():
     for on in (False, True):
         pm.zero_grad(set_to_none=True)
         x.grad = None
-        with options_override(ln_epilogue=on, ln_epilogue_tile=on), torch.autocast("cuda", dtype=torch.bfloat16):
+        with options_override(ln_epilogue=on, ln_epilogue_tile=on, merge_gemm=False), \
+                torch.autocast("cuda", dtype=torch.bfloat16):
             s = pm.forward_stream(sw.ResidualStream(x, x.bfloat16()))
         (s.f32.square().mean() + s.bf16.float().mean()).backward()
         outs.append((s.f32.detach(), s.bf16.detach(), {n: p.grad.clone() for n, p in pm.named_parameters()}))
