@@ -41,6 +41,9 @@ class GradientBuckets:
         # force: exchange even at world 1 (a one-rank RCCL group exercises the whole hook /
         # all-reduce / synchronize path on a one-GPU box, tests/test_gpu_ddp.py)
         self.enabled = self.world > 1 or (force and dist.is_initialized())
+        if self.enabled:  # the hooks read each gradient as it lands: no weight-gradient side stream
+            from . import ops
+            ops._WgradStream.allowed = False
         self.defer = False  # graph mode: no hook-launched all-reduce (allreduce_now() instead)
         # grad_accum: microbatches before the last only accumulate into the bucket views (no
         # arrival count, no all-reduce: composer's DDP no_sync)

@@ -169,7 +169,83 @@ def _gelu_recompute(M, K, N1, N2):
             and lib.hvk_weight_grad_gelu_x_supported(M, N2, N1))
 
 
+class _WgradStream:
+    """options.wgrad_stream state: the side stream, whether launches on it are not yet joined,
+    whether this backward's join callback is queued."""
+    side = None
+    pending = False
+    armed = False
+    allowed = True  # GradientBuckets turns it off (its hooks read each gradient as it lands)
+
+
+def _wgrad_fork():
+    """(main, side) when the weight-gradient side stream is in use for this launch, else None."""
+    if not (OPTIONS.wgrad_stream and _WgradStream.allowed):
+        return None
+    if _WgradStream.side is None:
+        _WgradStream.side = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    _WgradStream.side.wait_stream(main)
+    return main, _WgradStream.side
+
+
+def _wgrad_joined(tensors):
+    """After launches on the side stream that read / write `tensors` (allocated on the main
+    stream): keep their memory until the side stream is done with it, and make sure the main
+    stream waits for the side stream before the backward returns (an autograd final callback;
+    outside a backward, at once)."""
+    side = _WgradStream.side
+    for t in tensors:
+        if t is not None:
+            t.record_stream(side)
+    _WgradStream.pending = True
+    if not _WgradStream.armed:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_wgrad_join_callback)
+            _WgradStream.armed = True
+        except RuntimeError:  # not inside a backward pass
+            join_wgrad()
+
+
+def _wgrad_join_callback():
+    _WgradStream.armed = False
+    join_wgrad()
+
+
+def join_wgrad():
+    """The current stream waits for every weight-gradient launch on the side stream."""
+    if _WgradStream.pending:
+        torch.cuda.current_stream().wait_stream(_WgradStream.side)
+        _WgradStream.pending = False
+
+
 def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None):
+    """weight_grad_sync on the weight-gradient side stream (options.wgrad_stream, inside a
+    backward, libhvk's kernel for the shape) or the current one."""
+    lib = _lib.load()
+    M, N = g.shape
+    K = x.shape[1]
+    fork = _wgrad_fork() if g.is_cuda and (gelu_x or lib.hvk_weight_grad_supported(M, N, K)) else None
+    if fork is None:
+        return weight_grad_sync(g, x, with_db, gelu_x, xshift)
+    main, side = fork
+    dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
+    db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
+    nb = lib.hvk_weight_grad_workspace(M, N, K)
+    ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
+    xs = _f32(xshift) if xshift is not None else None
+    with torch.cuda.stream(side):
+        if gelu_x:
+            call("hvk_weight_grad_gelu_x", ptr(g), ptr(x), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
+        elif xs is not None:
+            call("hvk_weight_grad_shift", ptr(g), ptr(x), ptr(xs), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
+        else:
+            call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
+    _wgrad_joined((g, x, xs, dw, db, ws))
+    return dw, db
+
+
+def weight_grad_sync(g, x, with_db=False, gelu_x=False, xshift=None):
     """(dW, db) = (g^T x, g.sum(0)) in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to
     ~10^6): libhvk's token-chunked MFMA kernel with the bias gradient fused (hvk_weight_grad,
     one pass over g) for every SwinV2-T shape it is built for; otherwise the library GEMM
