@@ -4,6 +4,7 @@ Every Function here launches only HIP kernels from libhvk.so on PyTorch's
 current stream; tensors are plumbing (PyTorch owns the memory).  There is no
 eager/CPU fallback: a CPU tensor or a missing library raises.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -1406,7 +1407,11 @@ def _merge_linear_bwd(ctx, xb, wb, ga):
         nb = lib.hvk_weight_grad_workspace(M, N, 4 * C)
         ws = torch.empty(nb // 4, device=ga.device, dtype=torch.float32)
         dw = torch.empty((N, 4 * C), device=ga.device, dtype=torch.float32)
-        call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
+        fork = _wgrad_fork()  # options.wgrad_stream: on the weight-gradient side stream
+        with torch.cuda.stream(fork[1]) if fork else contextlib.nullcontext():
+            call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
+        if fork:
+            _wgrad_joined((ga, xb, dw, ws))
     return gx, dw
 
 
