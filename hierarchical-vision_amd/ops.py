@@ -839,10 +839,16 @@ class BlockTables(torch.autograd.Function):
         ws = _CPB_WS.get(key)
         if ws is None:
             ws = _CPB_WS[key] = torch.empty(nbytes // 4, device=w1.device, dtype=torch.float32)
-        call("hvk_block_bias_bwd", ptr(g_eff), ptr(v), ptr(pw), C, ptr(dpb), ptr(dv), ptr(dpw),
-             ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), ctx.clamp_max, RR, nH, hid, ptr(table),
-             ptr(dtable), ptr(dscale), ptr(dw1), ptr(db1), ptr(dw2), ptr(dlogit), ptr(ws), nbytes,
-             stream())
+        # parameter gradients only: on the weight-gradient side stream when enabled
+        fork = _wgrad_fork()
+        with torch.cuda.stream(fork[1]) if fork else contextlib.nullcontext():
+            call("hvk_block_bias_bwd", ptr(g_eff), ptr(v), ptr(pw), C, ptr(dpb), ptr(dv), ptr(dpw),
+                 ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), ctx.clamp_max, RR, nH, hid, ptr(table),
+                 ptr(dtable), ptr(dscale), ptr(dw1), ptr(db1), ptr(dw2), ptr(dlogit), ptr(ws), nbytes,
+                 stream())
+        if fork:
+            _wgrad_joined((g_eff, v, pw, coords, w1, b1, w2, logit, table, dtable, dscale, dpb, dv, dpw, dw1, db1,
+                           dw2, dlogit))
         return (dv, dpb, dpw, None, dw1, db1, dw2, dlogit.reshape(ctx.logit_shape), None, None)
 
 
