@@ -27,8 +27,12 @@ Design for MI355X:
   ``synchronize(scale=True)`` divides in place for optimizers that cannot take it.
 No other collective runs in the step.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
+
+from . import ops
 
 
 class GradientBuckets:
@@ -41,9 +45,6 @@ class GradientBuckets:
         # force: exchange even at world 1 (a one-rank RCCL group exercises the whole hook /
         # all-reduce / synchronize path on a one-GPU box, tests/test_gpu_ddp.py)
         self.enabled = self.world > 1 or (force and dist.is_initialized())
-        if self.enabled:  # the hooks read each gradient as it lands: no weight-gradient side stream
-            from . import ops
-            ops._WgradStream.allowed = False
         self.defer = False  # graph mode: no hook-launched all-reduce (allreduce_now() instead)
         # grad_accum: microbatches before the last only accumulate into the bucket views (no
         # arrival count, no all-reduce: composer's DDP no_sync)
@@ -117,22 +118,35 @@ class GradientBuckets:
 
     def _make_hook(self, bi):
         def hook(p):
-            v = self._view[p]
-            if p.grad is not v:  # the fresh gradient autograd handed over -> its bucket slot
-                v.copy_(p.grad)
-                p.grad = v
-            if self.accumulating:  # later microbatches add onto the view in place
-                return
-            self._pending[bi] -= 1
-            if self._pending[bi] == 0 and self.enabled and not self.defer:
-                flat = self.buckets[bi][0]
-                if self.trace is not None:
-                    ev = torch.cuda.Event(enable_timing=True)
-                    ev.record()
-                    self.trace.append((bi, ev))
-                self._works[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg,
-                                                  async_op=True)
+            # a gradient computed on the weight-gradient side stream (ops.wgrad_stream_scope)
+            # is copied, and its bucket's all-reduce issued, on that stream (after everything
+            # the current stream queued so far): the hook does not make the backward wait
+            side = ops.wgrad_side_pending() if p.is_cuda else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                self._hook_body(bi, p, side)
         return hook
+
+    def _hook_body(self, bi, p, side):
+        v = self._view[p]
+        if p.grad is not v:  # the fresh gradient autograd handed over -> its bucket slot
+            g = p.grad
+            v.copy_(g)
+            if side is not None:
+                g.record_stream(side)
+            p.grad = v
+        if self.accumulating:  # later microbatches add onto the view in place
+            return
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0 and self.enabled and not self.defer:
+            flat = self.buckets[bi][0]
+            if self.trace is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                self.trace.append((bi, ev))
+            self._works[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg,
+                                              async_op=True)
 
     def reset(self):
         """Before the next backward: every param.grad None (autograd hands the new gradient

@@ -171,17 +171,38 @@ def _gelu_recompute(M, K, N1, N2):
 
 
 class _WgradStream:
-    """options.wgrad_stream state: the side stream, whether launches on it are not yet joined,
-    whether this backward's join callback is queued."""
+    """options.wgrad_stream state: the side stream, whether a backward that allows it is running
+    (wgrad_stream_scope), whether launches on it are not yet joined, whether this backward's join
+    callback is queued."""
     side = None
+    active = False
     pending = False
     armed = False
-    allowed = True  # GradientBuckets turns it off (its hooks read each gradient as it lands)
 
 
-def _wgrad_fork():
-    """(main, side) when the weight-gradient side stream is in use for this launch, else None."""
-    if not (OPTIONS.wgrad_stream and _WgradStream.allowed):
+@contextlib.contextmanager
+def wgrad_stream_scope(enabled=True):
+    """Around a backward whose parameters all start with .grad None (the Trainer's, after its
+    bucket reset, one microbatch): parameter gradients may then be computed on the side stream
+    -- autograd hands a fresh leaf gradient over without reading it, and the stream is joined at
+    the end of the backward -- so they overlap the input-gradient chain (options.wgrad_stream).
+    Outside a scope, or for a parameter that already holds a gradient (accumulation), the launch
+    stays on the current stream."""
+    prev = _WgradStream.active
+    _WgradStream.active = enabled
+    try:
+        yield
+    finally:
+        _WgradStream.active = prev
+        join_wgrad()
+
+
+def _wgrad_fork(leaves):
+    """(main, side) when the gradients of `leaves` (the parameters the launch produces gradients
+    for) may be computed on the side stream, else None."""
+    if not (OPTIONS.wgrad_stream and _WgradStream.active and leaves) or torch.cuda.is_current_stream_capturing():
+        return None
+    if not all(t is None or (t.is_leaf and t.grad is None) for t in leaves):
         return None
     if _WgradStream.side is None:
         _WgradStream.side = torch.cuda.Stream()
@@ -220,13 +241,20 @@ def join_wgrad():
         _WgradStream.pending = False
 
 
-def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None):
-    """weight_grad_sync on the weight-gradient side stream (options.wgrad_stream, inside a
-    backward, libhvk's kernel for the shape) or the current one."""
+def wgrad_side_pending():
+    """The side stream while launches on it are not joined yet, else None (GradientBuckets'
+    hooks then copy each gradient into its bucket on it)."""
+    return _WgradStream.side if _WgradStream.pending else None
+
+
+def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None, leaves=()):
+    """weight_grad_sync, on the weight-gradient side stream when `leaves` (the parameters whose
+    gradients dW / db are) allow it (wgrad_stream_scope) and libhvk's kernel is built for the
+    shape, else on the current stream."""
     lib = _lib.load()
     M, N = g.shape
     K = x.shape[1]
-    fork = _wgrad_fork() if g.is_cuda and (gelu_x or lib.hvk_weight_grad_supported(M, N, K)) else None
+    fork = _wgrad_fork(leaves) if g.is_cuda and (gelu_x or lib.hvk_weight_grad_supported(M, N, K)) else None
     if fork is None:
         return weight_grad_sync(g, x, with_db, gelu_x, xshift)
     main, side = fork
@@ -392,6 +420,7 @@ class LinearFn(torch.autograd.Function):
         ctx.wt = wt
         ctx.has_bias = bias is not None
         ctx.xshift = xshift.detach() if xshift is not None else None
+        ctx.leaves = (weight, bias)
         return y
 
     @staticmethod
@@ -406,7 +435,8 @@ class LinearFn(torch.autograd.Function):
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = None, None
         if ctx.needs_input_grad[1]:
-            dw, db = weight_grad(g2, xb.reshape(-1, K), want_db, xshift=getattr(ctx, "xshift", None))
+            dw, db = weight_grad(g2, xb.reshape(-1, K), want_db, xshift=getattr(ctx, "xshift", None),
+                                 leaves=ctx.leaves if want_db or not ctx.has_bias else ())
         elif want_db:
             db = g2.sum(dim=0, dtype=torch.float32)
         return gx, dw, db, None
@@ -812,6 +842,7 @@ class BlockTables(torch.autograd.Function):
         ctx.has_pb = proj_bias is not None
         ctx.clamp_max = float(clamp_max)
         ctx.logit_shape = logit_scale.shape
+        ctx.leaves = (v_bias, proj_bias, proj_w, w1, b1, w2, logit_scale)
         ctx.mark_non_differentiable(qkv_bias)
         ctx.set_materialize_grads(False)
         return qkv_bias, eff, table, scale
@@ -840,7 +871,7 @@ class BlockTables(torch.autograd.Function):
         if ws is None:
             ws = _CPB_WS[key] = torch.empty(nbytes // 4, device=w1.device, dtype=torch.float32)
         # parameter gradients only: on the weight-gradient side stream when enabled
-        fork = _wgrad_fork()
+        fork = _wgrad_fork(ctx.leaves)
         with torch.cuda.stream(fork[1]) if fork else contextlib.nullcontext():
             call("hvk_block_bias_bwd", ptr(g_eff), ptr(v), ptr(pw), C, ptr(dpb), ptr(dv), ptr(dpw),
                  ptr(coords), ptr(w1), ptr(b1), ptr(w2), ptr(logit), ctx.clamp_max, RR, nH, hid, ptr(table),
@@ -949,6 +980,7 @@ class LinearLNFn(torch.autograd.Function):
              stream())
         ctx.save_for_backward(xin, wb, a, abias, gamma, sample_scale, mean, rstd)
         ctx.wt = wt
+        ctx.leaves = (weight,)
         ctx.xshift = xshift.detach() if xshift is not None else None
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
@@ -967,7 +999,8 @@ class LinearLNFn(torch.autograd.Function):
         gin = None
         if ctx.needs_input_grad[0]:
             gin = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K) else g2 @ wb).reshape(xin.shape)
-        dw = weight_grad(g2, xin.reshape(-1, K), False, xshift=ctx.xshift)[0] if ctx.needs_input_grad[1] else None
+        dw = (weight_grad(g2, xin.reshape(-1, K), False, xshift=ctx.xshift, leaves=ctx.leaves)[0]
+              if ctx.needs_input_grad[1] else None)
         return gin, dw, None, dabias, gx0, dgamma, dbeta, None, None, None
 
 
@@ -1074,6 +1107,7 @@ class LinearGelu(torch.autograd.Function):
         h, y = gelu_fwd(xb.reshape(-1, K), wb, bias)
         ctx.save_for_backward(xb, wb, h)
         ctx.wt = wt
+        ctx.leaves = (weight,)
         return y.reshape(*xb.shape[:-1], N)
 
     @staticmethod
@@ -1092,7 +1126,7 @@ class LinearGelu(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, _bf16_t(wb, ctx.wt)) if _native_nt(M, N, K)
                   else gh @ wb).reshape(xb.shape)
-        dw = weight_grad(gh, xb.reshape(-1, K))[0] if ctx.needs_input_grad[1] else None
+        dw = weight_grad(gh, xb.reshape(-1, K), leaves=ctx.leaves)[0] if ctx.needs_input_grad[1] else None
         return gx, dw, db
 
 
@@ -1146,6 +1180,7 @@ class MlpFn(torch.autograd.Function):
             y = mm_nt(y1, w2b, b2)
             ctx.save_for_backward(xb, w1b, w2b, h, y1)
         ctx.has_b2 = b2 is not None
+        ctx.leaves = ((w1, b1), (w2, b2))
         return y.reshape(*xb.shape[:-1], N2)
 
     @staticmethod
@@ -1159,9 +1194,9 @@ class MlpFn(torch.autograd.Function):
         g2 = _bf16(gy).reshape(-1, N2)
         M = g2.shape[0]
         if ctx.recompute:
-            dw2, db2 = weight_grad(g2, h, ctx.has_b2, gelu_x=True)
+            dw2, db2 = weight_grad(g2, h, ctx.has_b2, gelu_x=True, leaves=ctx.leaves[1])
         else:
-            dw2, db2 = weight_grad(g2, y1, ctx.has_b2)
+            dw2, db2 = weight_grad(g2, y1, ctx.has_b2, leaves=ctx.leaves[1])
         gh = torch.empty_like(h)
         w2t = _bf16_t(w2b, ctx.wts[1])
         if (OPTIONS.mlp_fused and ctx.needs_input_grad[0] and not ctx.recompute
@@ -1171,7 +1206,7 @@ class MlpFn(torch.autograd.Function):
             gx = torch.empty((M, K), device=h.device, dtype=torch.bfloat16)
             call("hvk_mlp_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(_bf16_t(w1b, ctx.wts[0])), ptr(gh), ptr(gx),
                  M, N2, N1, K, stream())
-            dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+            dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=ctx.leaves[0])  # fc1 bias gradient fused
             return gx.reshape(xb.shape), dw1, db1, dw2, db2
         if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
                                          _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
@@ -1183,7 +1218,7 @@ class MlpFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, _bf16_t(w1b, ctx.wts[0])) if _native_nt(M, N1, K)
                   else gh @ w1b).reshape(xb.shape)
-        dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+        dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=ctx.leaves[0])  # fc1 bias gradient fused
         return gx, dw1, db1, dw2, db2
 
 
@@ -1223,6 +1258,7 @@ class MlpLNFn(torch.autograd.Function):
                  ptr(rstd), stream())
         ctx.save_for_backward(xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd)
         ctx.wts = (w1t, w2t)
+        ctx.leaves = ((w1, b1), (w2,))
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
         ctx.set_materialize_grads(False)
@@ -1236,18 +1272,18 @@ class MlpLNFn(torch.autograd.Function):
             return (None,) * 11
         ga, dabias, gx0, dgamma, dbeta = r
         bwd = _mlp_bwd if ctx.fused else _mlp_bwd_tiled
-        gin, dw1, db1, dw2 = bwd(ga, xin, w1b, w2b, h, y1, ctx.wts, ctx.needs_input_grad[0])
+        gin, dw1, db1, dw2 = bwd(ga, xin, w1b, w2b, h, y1, ctx.wts, ctx.needs_input_grad[0], ctx.leaves)
         return gin, dw1, db1, dw2, dabias, gx0, dgamma, dbeta, None, None, None
 
 
-def _mlp_bwd(gy, xb, w1b, w2b, h, y1, wts, want_x):
+def _mlp_bwd(gy, xb, w1b, w2b, h, y1, wts, want_x, leaves=((), ())):
     """MlpFn's backward at the stage-0 width (the fused hvk_mlp_bwd chain; fc2's bias gradient is
     the caller's): (gx, dW1, db1, dW2)."""
     N1, K = w1b.shape
     N2 = w2b.shape[0]
     g2 = _bf16(gy).reshape(-1, N2)
     M = g2.shape[0]
-    dw2 = weight_grad(g2, y1)[0]
+    dw2 = weight_grad(g2, y1, leaves=leaves[1])[0]
     gh = torch.empty_like(h)
     w2t = _bf16_t(w2b, wts[1])
     gx = None
@@ -1258,11 +1294,11 @@ def _mlp_bwd(gy, xb, w1b, w2b, h, y1, wts, want_x):
         gx = gx.reshape(xb.shape)
     else:
         call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1, stream())
-    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=leaves[0])  # fc1 bias gradient fused
     return gx, dw1, db1, dw2
 
 
-def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x):
+def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x, leaves=((), ())):
     """MlpFn's unfused backward chain (fc2's input gradient through GELU' as one kernel, fc1's
     input gradient, both weight gradients; fc2's bias gradient is the caller's): (gx, dW1, db1,
     dW2)."""
@@ -1270,7 +1306,7 @@ def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x):
     N2 = w2b.shape[0]
     g2 = _bf16(gy).reshape(-1, N2)
     M = g2.shape[0]
-    dw2 = weight_grad(g2, y1)[0]
+    dw2 = weight_grad(g2, y1, leaves=leaves[1])[0]
     gh = torch.empty_like(h)
     w2t = _bf16_t(w2b, wts[1])
     if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
@@ -1281,7 +1317,7 @@ def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x):
     gx = None
     if want_x:
         gx = (mm_nt(gh, _bf16_t(w1b, wts[0])) if _native_nt(M, N1, K) else gh @ w1b).reshape(xb.shape)
-    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True)  # fc1 bias gradient fused
+    dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=leaves[0])  # fc1 bias gradient fused
     return gx, dw1, db1, dw2
 
 
@@ -1413,7 +1449,7 @@ def _merge_linear_bwd(ctx, xb, wb, ga):
         nb = lib.hvk_weight_grad_workspace(M, N, 4 * C)
         ws = torch.empty(nb // 4, device=ga.device, dtype=torch.float32)
         dw = torch.empty((N, 4 * C), device=ga.device, dtype=torch.float32)
-        fork = _wgrad_fork()  # options.wgrad_stream: on the weight-gradient side stream
+        fork = _wgrad_fork(ctx.leaves)  # options.wgrad_stream: on the weight-gradient side stream
         with torch.cuda.stream(fork[1]) if fork else contextlib.nullcontext():
             call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
         if fork:
@@ -1438,6 +1474,7 @@ class MergeLinearFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.wt = wt
         ctx.geo = (B, H, W, C, N)
+        ctx.leaves = (weight,)
         return y
 
     @staticmethod
@@ -1467,6 +1504,7 @@ class MergeLinearLNFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb, a, gamma, mean, rstd)
         ctx.wt = wt
         ctx.geo = (B, H, W, C, N)
+        ctx.leaves = (weight,)
         ctx.set_materialize_grads(False)
         return xo, xob
 

@@ -42,10 +42,11 @@ class HostOptions:
     # gradient scattered by the dgrad GEMM's store, the weight gradient gathering on its DMA:
     # no [T/4, 4C] tensor either way (hvk_merge_*, bit-identical)
     merge_gemm: bool = True
-    # weight-gradient GEMMs on a second HIP stream, forked at each launch and joined at the end
-    # of the backward (ops.weight_grad): they overlap the input-gradient chain instead of
-    # serialising behind it; single-rank only (GradientBuckets reads each gradient as it lands)
-    wgrad_stream: bool = False
+    # parameter-gradient launches (weight gradients, the block-bias backward) on a second HIP
+    # stream inside the Trainer's backward (ops.wgrad_stream_scope), joined at its end: they
+    # overlap the input-gradient chain instead of serialising behind it (+2.6 %, 3 interleaved
+    # runs, profiles/round5/wgrad_stream/ab.txt); GradientBuckets copies / all-reduces on it
+    wgrad_stream: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

@@ -13,6 +13,7 @@ The batch must live in the static tensors passed to capture() (copy new data int
 BATCH_END algorithms (EMA: host-side counters) run eagerly after the replays."""
 import torch
 
+from . import ops
 from .algorithmic import Event, State
 from .ddp import GradientBuckets
 
@@ -93,7 +94,10 @@ class Trainer:
             self._run(Event.AFTER_LOSS)
             if len(micro) > 1:
                 st.loss = st.loss * (1.0 / len(micro))
-            st.loss.backward()
+            # parameter gradients may run on the weight-gradient side stream (ops.wgrad_stream_scope:
+            # a parameter still holding a gradient, i.e. a later microbatch, stays on this stream)
+            with ops.wgrad_stream_scope(dev_type == "cuda"):
+                st.loss.backward()
             total = st.loss.detach() if total is None else total + st.loss.detach()
         self.buckets.accumulating = False
         st.batch = batch
