@@ -99,6 +99,8 @@ SIGNATURES = {
     "hvk_ln_bwd_workspace_bytes": (_sz, [_i]),
     "hvk_ln_residual_bwd": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
                                  _p, _sz, _p]),
+    "hvk_ln_residual_bwd_split": (_i, [_p, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p,
+                                       _p, _sz, _p, _p]),
     "hvk_bias_gelu_fwd": (_i, [_p, _p, _p, _i, _i, _p]),
     "hvk_bias_gelu_bwd_workspace_bytes": (_sz, [_i]),
     "hvk_bias_gelu_bwd": (_i, [_p, _p, _p, _p, _p, _p, _sz, _i, _i, _p]),
@@ -117,7 +119,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 12  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
+ABI_VERSION = 13  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
 
 
 def load():

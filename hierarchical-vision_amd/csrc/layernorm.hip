@@ -473,11 +473,33 @@ int hvk_ln_residual_fwd(const void* a, const float* abias, const float* x0, cons
 
 size_t hvk_ln_bwd_workspace_bytes(int C) { return (size_t)kBwdBlocks * 3 * C * sizeof(float); }
 
+static int ln_residual_bwd(const void* a, const float* abias, const float* gamma, const float* sample_scale,
+                           const float* mean, const float* rstd, const float* gx, const void* gxb, int rows, int C,
+                           int rows_per_sample, float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
+                           float* workspace, size_t workspace_bytes, void* stream, void* param_stream);
+
 int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
                         const float* sample_scale, const float* mean, const float* rstd,
                         const float* gx, const void* gxb, int rows, int C, int rows_per_sample,
                         float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
                         float* workspace, size_t workspace_bytes, void* stream) {
+  return ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, gx, gxb, rows, C, rows_per_sample, gx0, ga,
+                         dgamma, dbeta, dabias, workspace, workspace_bytes, stream, nullptr);
+}
+
+int hvk_ln_residual_bwd_split(const void* a, const float* abias, const float* gamma, const float* sample_scale,
+                              const float* mean, const float* rstd, const float* gx, const void* gxb, int rows,
+                              int C, int rows_per_sample, float* gx0, void* ga, float* dgamma, float* dbeta,
+                              float* dabias, float* workspace, size_t workspace_bytes, void* stream,
+                              void* param_stream) {
+  return ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, gx, gxb, rows, C, rows_per_sample, gx0, ga,
+                         dgamma, dbeta, dabias, workspace, workspace_bytes, stream, param_stream);
+}
+
+static int ln_residual_bwd(const void* a, const float* abias, const float* gamma, const float* sample_scale,
+                           const float* mean, const float* rstd, const float* gx, const void* gxb, int rows, int C,
+                           int rows_per_sample, float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
+                           float* workspace, size_t workspace_bytes, void* stream, void* param_stream) {
   int ept, tpr;
   int rc = check_shape("hvk_ln_residual_bwd", rows, C, rows_per_sample, ept, tpr);
   if (rc) return rc;
@@ -494,7 +516,18 @@ int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
           static_cast<hvk_bf16*>(ga), workspace, dgamma, dbeta, dabias};
   HVK_LN_DISPATCH(ln_bwd_kernel, dim3(grid), st, p);
   HVK_CHECK_LAUNCH("ln_bwd");
-  hipLaunchKernelGGL(colsum_kernel, dim3((3 * C + 63) / 64, kRedRowGroups), dim3(64), 0, st,
+  hipStream_t cs = st;
+  if (param_stream && param_stream != stream) {
+    // the column sums (parameter gradients only) on the caller's parameter-gradient stream,
+    // ordered after the row kernel by an event: they overlap the next input-gradient launches
+    static hipEvent_t ev = nullptr;
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd_split: event create failed");
+    cs = static_cast<hipStream_t>(param_stream);
+    if (hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(cs, ev, 0) != hipSuccess)
+      return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd_split: stream ordering failed");
+  }
+  hipLaunchKernelGGL(colsum_kernel, dim3((3 * C + 63) / 64, kRedRowGroups), dim3(64), 0, cs,
                      workspace, grid, 3 * C, dgamma, dbeta, dabias, C);
   HVK_CHECK_LAUNCH("ln_bwd_colsum");
   return HVK_OK;

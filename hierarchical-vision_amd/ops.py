@@ -895,6 +895,7 @@ class LayerNormResidual(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, a, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        abias_p, gamma_p, beta_p = abias, gamma, beta
         C = a.shape[-1]
         rows = a.numel() // C
         a = _bf16(a)
@@ -910,6 +911,7 @@ class LayerNormResidual(torch.autograd.Function):
              ptr(sample_scale), rows, C, rows_per_sample, float(eps), ptr(x), ptr(xb), ptr(mean),
              ptr(rstd), stream())
         ctx.save_for_backward(a, abias, gamma, sample_scale, mean, rstd)
+        ctx.ln_leaves = (abias_p, gamma_p, beta_p)
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
         # an unused output (e.g. the bf16 copy at a stage end) gets None, not a zero-filled
@@ -920,16 +922,18 @@ class LayerNormResidual(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, gxb):
         a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
-        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb, ctx.ln_leaves)
         if r is None:
             return (None,) * 8
         ga, dabias, gx0, dgamma, dbeta = r
         return ga, dabias, gx0, dgamma, dbeta, None, None, None
 
 
-def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx, gxb):
+def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx, gxb, leaves=()):
     """Backward of x = x0 + s (gamma * LN(a + abias) + beta) (hvk_ln_residual_bwd): (ga, dabias,
-    gx0, dgamma, dbeta), or None when neither output has a gradient."""
+    gx0, dgamma, dbeta), or None when neither output has a gradient.  `leaves`: the parameters
+    (abias, gamma, beta) whose gradients the column sums are; where they allow it
+    (wgrad_stream_scope) the sums run on the side stream (hvk_ln_residual_bwd_split)."""
     C = a.shape[-1]
     rows = a.numel() // C
     gx = _f32(gx) if gx is not None else None
@@ -943,9 +947,16 @@ def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx,
     dabias = torch.empty_like(gamma) if abias is not None else None
     ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
     ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
-    call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
+    fork = _wgrad_fork(leaves) if a.is_cuda else None
+    if fork is None:
+        call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
+             ptr(rstd), ptr(gx), ptr(gxb), rows, C, rps, ptr(gx0), ptr(ga), ptr(dgamma),
+             ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream())
+        return ga, dabias, gx0, dgamma, dbeta
+    call("hvk_ln_residual_bwd_split", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
          ptr(rstd), ptr(gx), ptr(gxb), rows, C, rps, ptr(gx0), ptr(ga), ptr(dgamma),
-         ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream())
+         ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream(), ctypes.c_void_p(fork[1].cuda_stream))
+    _wgrad_joined((ws, dgamma, dbeta, dabias))
     return ga, dabias, gx0, dgamma, dbeta
 
 
@@ -965,6 +976,7 @@ class LinearLNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, inp, weight, xshift, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        ctx.ln_leaves = (abias, gamma, beta)
         xin = _bf16(inp)
         wb, wt = _bf16_weight(weight)
         N, K = wb.shape
@@ -990,7 +1002,7 @@ class LinearLNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, gxb):
         xin, wb, a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
-        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb, ctx.ln_leaves)
         if r is None:
             return (None,) * 10
         ga, dabias, gx0, dgamma, dbeta = r
@@ -1232,6 +1244,7 @@ class MlpLNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, inp, w1, b1, w2, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
+        ctx.ln_leaves = (abias, gamma, beta)
         xin = _bf16(inp)
         w1b, w1t = _bf16_weight(w1)
         w2b, w2t = _bf16_weight(w2)
@@ -1267,7 +1280,7 @@ class MlpLNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, gxb):
         xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd = ctx.saved_tensors
-        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb)
+        r = _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, ctx.rps, ctx.has_x0, gx, gxb, ctx.ln_leaves)
         if r is None:
             return (None,) * 11
         ga, dabias, gx0, dgamma, dbeta = r
@@ -1491,6 +1504,7 @@ class MergeLinearLNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, eps, H, W):
+        ctx.ln_leaves = (gamma, beta)
         xb = _bf16(x).contiguous()
         wb, wt = _bf16_weight(weight)
         B, L, C = xb.shape
@@ -1511,7 +1525,7 @@ class MergeLinearLNFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gx, gxb):
         xb, wb, a, gamma, mean, rstd = ctx.saved_tensors
-        r = _ln_residual_bwd(a, None, gamma, None, mean, rstd, 1, False, gx, gxb)
+        r = _ln_residual_bwd(a, None, gamma, None, mean, rstd, 1, False, gx, gxb, ctx.ln_leaves)
         if r is None:
             return (None,) * 7
         ga, _, _, dgamma, dbeta = r

@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 /* the C ABI this header describes; hvk_abi_version() returns it (bindings check it at load) */
-#define HVK_ABI_VERSION 12
+#define HVK_ABI_VERSION 13
 
 #define HVK_OK 0
 #define HVK_EINVAL 1
@@ -372,6 +372,14 @@ int hvk_ln_residual_bwd(const void* a, const float* abias, const float* gamma,
                         const float* gx, const void* gxb, int rows, int C, int rows_per_sample,
                         float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
                         float* workspace, size_t workspace_bytes, void* stream);
+/* The same with the dgamma / dbeta / dabias column sums launched on param_stream (ordered after
+ * the row kernel on `stream` by an event; NULL or == stream: as above), so the parameter
+ * gradients overlap the input-gradient chain.  ABI 13. */
+int hvk_ln_residual_bwd_split(const void* a, const float* abias, const float* gamma, const float* sample_scale,
+                              const float* mean, const float* rstd, const float* gx, const void* gxb, int rows,
+                              int C, int rows_per_sample, float* gx0, void* ga, float* dgamma, float* dbeta,
+                              float* dabias, float* workspace, size_t workspace_bytes, void* stream,
+                              void* param_stream);
 
 /* Final LayerNorm + token average pool (swinv2.py:833-835): y [B, C] = mean over T of
  * LN(x [B, T, C] f32) (eps, gamma, beta).  The forward keeps xsum [B, C] = sum_t xhat and
