@@ -947,7 +947,7 @@ def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx,
     dabias = torch.empty_like(gamma) if abias is not None else None
     ws_bytes = _lib.load().hvk_ln_bwd_workspace_bytes(C)
     ws = torch.empty(ws_bytes // 4, device=a.device, dtype=torch.float32)
-    fork = _wgrad_fork(leaves) if a.is_cuda else None
+    fork = _wgrad_fork(leaves) if a.is_cuda and OPTIONS.wgrad_stream_ln else None
     if fork is None:
         call("hvk_ln_residual_bwd", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
              ptr(rstd), ptr(gx), ptr(gxb), rows, C, rps, ptr(gx0), ptr(ga), ptr(dgamma),

@@ -47,6 +47,8 @@ class HostOptions:
     # overlap the input-gradient chain instead of serialising behind it (+2.6 %, 3 interleaved
     # runs, profiles/round5/wgrad_stream/ab.txt); GradientBuckets copies / all-reduces on it
     wgrad_stream: bool = True
+    # ... including the LayerNorm backward's parameter column sums (hvk_ln_residual_bwd_split)
+    wgrad_stream_ln: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward
