@@ -47,8 +47,10 @@ class HostOptions:
     # overlap the input-gradient chain instead of serialising behind it (+2.6 %, 3 interleaved
     # runs, profiles/round5/wgrad_stream/ab.txt); GradientBuckets copies / all-reduces on it
     wgrad_stream: bool = True
-    # ... including the LayerNorm backward's parameter column sums (hvk_ln_residual_bwd_split)
-    wgrad_stream_ln: bool = True
+    # ... including the LayerNorm backward's parameter column sums (hvk_ln_residual_bwd_split):
+    # off, measured -1.5 % against the side stream without them (3 interleaved runs,
+    # profiles/round5/wgrad_stream/ab_ln.txt)
+    wgrad_stream_ln: bool = False
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward
