@@ -122,8 +122,8 @@ class GradientBuckets:
             # is copied, and its bucket's all-reduce issued, on that stream (after everything
             # the current stream queued so far): the hook does not make the backward wait
             side = ops.wgrad_side_pending() if p.is_cuda else None
-            if side is not None:
-                side.wait_stream(torch.cuda.current_stream())
+            if side is not None and not ops.wgrad_produced_on_side(p.grad):
+                side.wait_stream(torch.cuda.current_stream())  # a gradient the current stream wrote
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
                 self._hook_body(bi, p, side)
         return hook

@@ -6,6 +6,7 @@ eager/CPU fallback: a CPU tensor or a missing library raises.
 """
 import contextlib
 import ctypes
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -178,6 +179,7 @@ class _WgradStream:
     active = False
     pending = False
     armed = False
+    produced = weakref.WeakSet()  # gradients written on the side stream (GradientBuckets' hooks)
 
 
 @contextlib.contextmanager
@@ -209,6 +211,19 @@ def _wgrad_fork(leaves):
     main = torch.cuda.current_stream()
     _WgradStream.side.wait_stream(main)
     return main, _WgradStream.side
+
+
+def _wgrad_outputs(*ts):
+    """Mark gradients a side-stream launch wrote (wgrad_produced_on_side)."""
+    for t in ts:
+        if t is not None:
+            _WgradStream.produced.add(t)
+
+
+def wgrad_produced_on_side(t):
+    """True for a gradient a side-stream launch wrote: a consumer on the side stream needs no
+    wait for the current stream to read it."""
+    return t in _WgradStream.produced
 
 
 def _wgrad_joined(tensors):
@@ -271,6 +286,7 @@ def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None, leaves=()):
         else:
             call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
     _wgrad_joined((g, x, xs, dw, db, ws))
+    _wgrad_outputs(dw, db)
     return dw, db
 
 
@@ -880,6 +896,7 @@ class BlockTables(torch.autograd.Function):
         if fork:
             _wgrad_joined((g_eff, v, pw, coords, w1, b1, w2, logit, table, dtable, dscale, dpb, dv, dpw, dw1, db1,
                            dw2, dlogit))
+            _wgrad_outputs(dv, dpb, dpw, dw1, db1, dw2)
         return (dv, dpb, dpw, None, dw1, db1, dw2, dlogit.reshape(ctx.logit_shape), None, None)
 
 
@@ -1467,6 +1484,7 @@ def _merge_linear_bwd(ctx, xb, wb, ga):
             call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
         if fork:
             _wgrad_joined((ga, xb, dw, ws))
+            _wgrad_outputs(dw)
     return gx, dw
 
 
