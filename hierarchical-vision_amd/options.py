@@ -45,7 +45,7 @@ class HostOptions:
     # parameter-gradient launches (weight gradients, the block-bias backward) on a second HIP
     # stream inside the Trainer's backward (ops.wgrad_stream_scope), joined at its end: they
     # overlap the input-gradient chain instead of serialising behind it (+2.6 %, 3 interleaved
-    # runs, profiles/round5/wgrad_stream/ab.txt); GradientBuckets copies / all-reduces on it
+    # runs, profiles/round5/wgrad_stream/ab.txt); the Trainer opens the scope for a single rank
     wgrad_stream: bool = True
     # ... including the LayerNorm backward's parameter column sums (hvk_ln_residual_bwd_split):
     # off, measured -1.5 % against the side stream without them (3 interleaved runs,

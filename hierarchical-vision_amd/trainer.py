@@ -94,9 +94,12 @@ class Trainer:
             self._run(Event.AFTER_LOSS)
             if len(micro) > 1:
                 st.loss = st.loss * (1.0 / len(micro))
-            # parameter gradients may run on the weight-gradient side stream (ops.wgrad_stream_scope:
-            # a parameter still holding a gradient, i.e. a later microbatch, stays on this stream)
-            with ops.wgrad_stream_scope(dev_type == "cuda"):
+            # single rank: parameter gradients may run on the weight-gradient side stream
+            # (ops.wgrad_stream_scope; a parameter still holding a gradient, i.e. a later
+            # microbatch, stays on this stream).  Not with the bucketed all-reduce: a bucket can
+            # only start once the side stream, which runs behind, has produced it (the dp2 gloo
+            # rehearsal measured -8 %, profiles/round5/wgrad_stream/dp2_ab.txt)
+            with ops.wgrad_stream_scope(dev_type == "cuda" and not self.buckets.enabled):
                 st.loss.backward()
             total = st.loss.detach() if total is None else total + st.loss.detach()
         self.buckets.accumulating = False
