@@ -60,6 +60,8 @@ def parse():
                     help="graph mode: eager warm-up steps whose W-MSA launches are timed")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="set a libhvk option (include/hvk.h hvk_set_option) before the run; A/B runs")
+    ap.add_argument("--stream-priority", type=int, default=0,
+                    help="run on a stream of this priority (negative = higher than the side stream's)")
     ap.add_argument("--host-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="set a host routing option (hvamd.options) before the run; A/B runs")
     return ap.parse_args()
@@ -352,6 +354,10 @@ def main():
         _lib.set_option(name, int(val))
     for o in args.host_opt:
         options.set(**options.parse(o))
+    if args.stream_priority:
+        # the whole run on a stream of this priority (negative = higher), the parameter-gradient
+        # side stream staying at the default: the input-gradient chain dispatches first
+        torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=args.stream_priority))
 
     cfg, tax, model, trainer = build(args, device)
     img = model.module.patch_embed.img_size[0]
