@@ -153,7 +153,7 @@ def load():
 
 # the library's named options (include/hvk.h, hvk_set_option); bench.py prints options()
 LIB_OPTIONS = ("wmsa_fwd_form", "wmsa_bwd_nt", "wmsa_bwd_slice_bytes", "gemm_pp", "tile_wide", "dw_tile",
-               "gemm_xr", "gemm_wide", "wmsa_fwd_hg")
+               "gemm_xr", "gemm_wide", "wmsa_fwd_hg", "dw_chunks")
 
 
 def options():

@@ -41,6 +41,7 @@ OptDef g_opts[HVK_OPT_COUNT] = {
     {"gemm_xr", 0, 0, 2},
     {"gemm_wide", 0, 0, 1},
     {"wmsa_fwd_hg", 0, 0, 6},
+    {"dw_chunks", 256, 16, 1024},
 };
 int find_opt(const char* name) {
   if (!name) return -1;

@@ -316,7 +316,8 @@ bool plan(int M, int N, int K, Plan& p) {
   p.ntk = K / p.tk;
   p.ntiles = p.ntk * (N / p.tn);
   p.nslices = M / TOK;
-  int nc = (p.var == V_T8C || p.var == V_B128 ? 512 : 256) / p.ntiles;
+  const int target = (int)hvk_opt(HVK_OPT_DW_CHUNKS);  // default 256: about one workgroup per CU
+  int nc = (p.var == V_T8C || p.var == V_B128 ? 2 * target : target) / p.ntiles;
   if (nc < 1) nc = 1;
   if (nc > p.nslices) nc = p.nslices;
   p.nchunk = nc;

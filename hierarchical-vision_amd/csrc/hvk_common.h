@@ -35,6 +35,7 @@ enum HvkOption {
   HVK_OPT_GEMM_XR,              // tiled GEMM: persistent row-range kernel where it fits (1, 2: DMA interleaved), 0 off
   HVK_OPT_GEMM_WIDE,            // tiled GEMM: 1 the 208 x 384 whole-row tile where built (gemm_wide.hip), 0 off
   HVK_OPT_WMSA_FWD_HG,          // w <= 8 forward (win form): heads per workgroup, 0 by head count, else 1 / 2 / 3 / 4 / 6
+  HVK_OPT_DW_CHUNKS,            // weight gradient: workgroup target per launch (token chunks = target / output tiles)
   HVK_OPT_COUNT
 };
 long long hvk_opt(int id);

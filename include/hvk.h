@@ -51,9 +51,13 @@ const char* hvk_last_error_string(void);
  *   gemm_wide             tiled GEMM (epilogues 0 / 1 / 2 / 4): 1 the 208 x 384 whole-row tile,
  *                         one 512-thread workgroup per CU (gemm_wide.hip; bit-identical) where
  *                         built (N % 384, K % 32, M >= 1664), 0 the 128-row tiles
- *   wmsa_fwd_hg           w <= 8 forward, win form: heads per workgroup; 0 (default) 3 where it
- *                         divides the head count, else 2, else 1; 1 / 2 / 3 / 4 / 6 force it where it
- *                         divides (the same results bit for bit: per-head math unchanged) */
+ *   wmsa_fwd_hg           w <= 8 forward, win form: heads per workgroup; 0 (default) 2 at 6 heads,
+ *                         else 3 where it divides the head count, else 2, else 1; 1 / 2 / 3 / 4 / 6
+ *                         force it where it divides (the same results bit for bit: per-head math
+ *                         unchanged)
+ *   dw_chunks             weight gradient: workgroups per launch to aim for (token chunks = this /
+ *                         output tiles, x2 for the 128 x 128 tiles; default 256: one per CU); the
+ *                         f32 partial sums change order with it */
 int hvk_set_option(const char* name, long long value, long long* previous);
 int hvk_get_option(const char* name, long long* value);
 

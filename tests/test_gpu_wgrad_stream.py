@@ -52,3 +52,27 @@ def test_accumulated_grads_equal_with_side_stream():
     blk = _block(96, 3)
     x = torch.randn(4, 28 * 28, 96, device="cuda")
     _compare(_grads(blk, x, False, passes=2), _grads(blk, x, True, passes=2))
+
+
+@pytest.mark.parametrize("chunks", [64, 128, 512])
+@pytest.mark.parametrize("M,N,K", [(50176, 384, 1536), (802816 // 8, 96, 384)])
+def test_weight_grad_chunk_target(chunks, M, N, K):
+    """libhvk option dw_chunks (workgroups per weight-gradient launch): another token-chunk count
+    only reorders the f32 partial sums -- dW / db against the f64 reference."""
+    from hvamd import _lib
+    g = torch.Generator(device="cuda").manual_seed(M + chunks)
+    gy = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    ref = gy.double().t() @ x.double()
+    with _lib.option("dw_chunks", chunks):
+        L = _lib.load()
+        nb = L.hvk_weight_grad_workspace(M, N, K)
+        ws = torch.empty(nb // 4, device="cuda")
+        dw = torch.empty(N, K, device="cuda")
+        db = torch.empty(N, device="cuda")
+        _lib.call("hvk_weight_grad", _lib.ptr(gy), _lib.ptr(x), _lib.ptr(dw), _lib.ptr(db), M, N, K, _lib.ptr(ws),
+                  nb, _lib.stream())
+        torch.cuda.synchronize()
+    assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
+    dbr = gy.double().sum(0)
+    assert ((db.double() - dbr).norm() / dbr.norm()).item() < 1e-6
