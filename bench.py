@@ -64,6 +64,9 @@ def parse():
                     help="run on a stream of this priority (negative = higher than the side stream's)")
     ap.add_argument("--host-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="set a host routing option (hvamd.options) before the run; A/B runs")
+    ap.add_argument("--comm-steps", type=int, default=5,
+                    help="world > 1: extra eager steps after the timed region that record the "
+                         "exchange's exposed time and bucket enqueue points (the `comm` block)")
     return ap.parse_args()
 
 
@@ -397,6 +400,21 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    fallbacks = ops.library_fallbacks(reset=True)  # warm-up + timed steps
+    comm = None
+    if world > 1 and not args.graph and args.comm_steps > 0:
+        # the exchange's exposed time and each bucket's overlap window, on extra steps after the
+        # timed region (Trainer.comm_timing: marks at the backward's start / end, each all-reduce
+        # enqueue, and after buckets.synchronize())
+        from hvamd.trainer import comm_report
+        trainer.comm_timing = []
+        for _ in range(args.comm_steps):
+            step()
+        comm = comm_report(trainer.comm_timing)
+        trainer.comm_timing = None
+        t = torch.tensor([comm["exposed_ms"], comm["exposed_ms_max"]], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        comm["exposed_ms_max_over_ranks"] = round(t[0].item(), 3)
     gemm_timer, gemm_steps, gemm_shapes = None, 0, None
     if timing and not args.graph:
         # the kernel timers run over extra steps after the timed region, so `value` is a clean
@@ -450,9 +468,14 @@ def main():
         "value_per_gpu": round(value / world, 2),
         "comm": ({"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                   "grad_buckets": len(trainer.buckets.buckets),
-                  "grad_bytes_per_step": 4 * sum(b[0].numel() for b in trainer.buckets.buckets)}
+                  "grad_bytes_per_step": 4 * sum(b[0].numel() for b in trainer.buckets.buckets),
+                  "bucket_mb": [round(b[0].numel() * 4 / 2**20, 1) for b in trainer.buckets.buckets],
+                  "wgrad_side_stream": bool(options.OPTIONS.wgrad_stream and options.OPTIONS.wgrad_stream_multi_rank),
+                  **(comm or {})}
                  if world > 1 else None),
         "final_loss": round(loss_val, 4),
+        # launches that left libhvk for a torch / hipBLASLt op over the warm-up + timed steps
+        "library_fallbacks": {"steps": args.warmup + args.steps, "sites": fallbacks},
         # every routing switch the run used: host (hvamd.options) and library (hvk_set_option)
         "options": {"host": options.as_dict(), "lib": _lib.options()},
         # whole-step MFMA utilisation: 3 x 2 x MACs per image (forward + both backward GEMMs)

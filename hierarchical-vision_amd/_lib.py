@@ -52,7 +52,6 @@ SIGNATURES = {
     "hvk_gemm_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_gelu_fwd": (_i, [_p, _p, _p, _p, _p, _i, _i, _i, _p]),
     "hvk_gemm_gelu_bwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
-    "hvk_gemm_set_pp": (_i, [_i]),
     "hvk_weight_grad_supported": (_i, [_i, _i, _i]),
     "hvk_head_supported": (_i, [_i, _i, _i]),
     "hvk_head_fwd": (_i, [_p, _p, _p, _p, _i, _i, _i, _p]),
@@ -119,7 +118,7 @@ SIGNATURES = {
 }
 
 _lib = None
-ABI_VERSION = 13  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
+ABI_VERSION = 14  # include/hvk.h's HVK_ABI_VERSION, the ABI this binding's SIGNATURES describe
 
 
 def load():
@@ -152,8 +151,8 @@ def load():
 
 
 # the library's named options (include/hvk.h, hvk_set_option); bench.py prints options()
-LIB_OPTIONS = ("wmsa_fwd_form", "wmsa_bwd_nt", "wmsa_bwd_slice_bytes", "gemm_pp", "tile_wide", "dw_tile",
-               "gemm_xr", "gemm_wide", "wmsa_fwd_hg", "dw_chunks")
+LIB_OPTIONS = ("wmsa_fwd_form", "wmsa_bwd_nt", "wmsa_bwd_slice_bytes", "tile_wide", "dw_tile", "wmsa_fwd_hg",
+               "dw_chunks")
 
 
 def options():

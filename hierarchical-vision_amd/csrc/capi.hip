@@ -35,11 +35,8 @@ OptDef g_opts[HVK_OPT_COUNT] = {
     {"wmsa_fwd_form", 0, 0, 1},
     {"wmsa_bwd_nt", 0, 0, 2},
     {"wmsa_bwd_slice_bytes", 1ll << 31, 1, 1ll << 31},
-    {"gemm_pp", 0, 0, 3},
     {"tile_wide", -1, -1, 1},
     {"dw_tile", 5, 4, 8},
-    {"gemm_xr", 0, 0, 2},
-    {"gemm_wide", 0, 0, 1},
     {"wmsa_fwd_hg", 0, 0, 6},
     {"dw_chunks", 256, 16, 1024},
 };

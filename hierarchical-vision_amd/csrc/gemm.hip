@@ -20,7 +20,7 @@
 #include <stdlib.h>
 
 #include "hvk_common.h"
-#include "gemm_xr.h"
+#include "gemm_tile_ln.h"
 
 namespace {
 

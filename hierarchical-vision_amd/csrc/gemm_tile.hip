@@ -14,7 +14,7 @@
 //    (as gemm.hip), so a lane ends with 8 consecutive output columns of one row: 16-B stores.
 #include <stdlib.h>
 
-#include "gemm_xr.h"
+#include "gemm_tile_ln.h"
 #include "hvk_common.h"
 
 // experiment builds (tools/probe/Makefile, NOT the product): 1 no MFMA, 2 no stores, 3 no DMA,
@@ -566,231 +566,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const hvk_bf16* __restr
 #endif
 }
 
-// ---- ping-pong tiled GEMM (one 512-thread workgroup per CU) ---------------------------------
-// The kernel above runs two barriers per 64-deep k-step with all of a workgroup's waves in the
-// same state: they wait for the stage together, read fragments together, then all issue MFMAs,
-// so the L2->LDS stream, the LDS reads and the MFMAs take turns (the k-step measured 0.77 us
-// against 0.43 us of MFMA work).  Here 8 waves form two groups of 4 that run the SAME phase
-// sequence one barrier apart: a phase is [fragment reads + LDS-DMA issue] barrier [16 MFMAs]
-// barrier, so while one group's MFMAs run on a SIMD the other group's wave on that SIMD reads
-// and issues DMA (s_setprio 1 over each MFMA cluster).  Group g owns tokens g*16*WTM .. +16*WTM
-// of the tile, wave c of a group owns columns c*16*WTN .. +16*WTN; a k-step is 4 phases, one
-// per quadrant (token half x column half) of the wave's tile, visited (0,0) (0,1) (1,1) (1,0) so
-// that every fragment is read once per k-step.  Tiles: 256 x 256 (WTM 8, WTN 4) and 128 x 384
-// (WTM 4, WTN 6), both 64 KB per k-step stage, two stages (128 KB).  The next k-step's stage is
-// DMA'd during phases 1-3 of this one and waited (own vmcnt(0)) in phase 4, one barrier before
-// the other group first reads it; a stage is overwritten only after phase 3 of both groups,
-// which hold every fragment of it in registers by then (their reads are waited before their
-// MFMAs, i.e. before the next barrier).
-template <int EPI, int WTM, int WTN>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(const hvk_bf16* __restrict__ X,
-                                                       const hvk_bf16* __restrict__ Wt,
-                                                       const float* __restrict__ bias,
-                                                       hvk_bf16* __restrict__ Y,
-                                                       hvk_bf16* __restrict__ Y2, int M, int N, int K,
-                                                       int mtiles) {
-  constexpr int BMP = 32 * WTM, BNP = 64 * WTN;  // tile tokens x columns
-  constexpr int STAGE = (BMP + BNP) * 128;       // bytes per 64-deep k-step
-  constexpr int NI = (BMP + BNP) / 64;           // DMA wave-instructions per wave and stage (8)
-  static_assert(NI == 8, "stage split assumes 8 DMA instructions per wave");
-  constexpr int HM = WTM / 2, HN = WTN / 2;      // quadrant tiles
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ntiles = N / BNP;
-  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-  const int nt = loc % ntiles, mt = (loc / ntiles) * 8 + xcd;
-  if (mt >= mtiles) return;
-  const int m0 = mt * BMP, n0 = nt * BNP;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int grp = wave >> 2, wc = wave & 3;
-  const int li = lane & 15, gq = lane >> 4;
-  const int KT = K / BK;
-
-  // A stage is refilled per REGION, two phases after the region's last fragment read (the
-  // other group reads it one barrier later): R1 = the first token half of each group's X rows
-  // + the first column half of each wave's W rows (read in phase 0), R2 = the second column
-  // halves (phase 1), R3 = the second token halves (phase 2).  K-step kt+2's R1 / R2 are
-  // issued in phases 2 / 3 of kt and its R3 in phase 0 of kt+1, so each region has ~1.5
-  // k-steps to land.  A region is a list of 8-row blocks (one 1-KB DMA wave-instruction each),
-  // block i of a list loaded by wave i % 8: R1 2WTM + 4WTN = 32 blocks (4 per wave), R2 4WTN,
-  // R3 2WTM (8 per wave in all).  Lane L of a block -> image row 8b + L/8, LDS chunk L%8 <-
-  // global chunk (L%8) ^ (L/8).
-  constexpr int N2 = WTN / 2, N3 = WTM / 4;  // R2 / R3 instructions per wave (R1: 4)
-  static_assert(4 * WTN == 8 * N2 && 2 * WTM == 8 * N3 && 2 * WTM + 4 * WTN == 32, "region split");
-  const int lr = lane >> 3, lc = lane & 7;
-  uint32_t src[NI], dst[NI];
-  bool isx[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    int blk;  // X block (< 2 * 2WTM... image rows / 8) or W block (+ BMP / 8)
-    if (i < 4) {  // R1: X first halves (group 0, 1), then W first halves (waves 0..3)
-      const int q = wave + 8 * i;
-      if (q < 2 * WTM) blk = (q / WTM) * 2 * WTM + q % WTM;
-      else { const int r = q - 2 * WTM; blk = BMP / 8 + (r / WTN) * 2 * WTN + r % WTN; }
-    } else if (i < 4 + N2) {  // R2: W second halves
-      const int r = wave + 8 * (i - 4);
-      blk = BMP / 8 + (r / WTN) * 2 * WTN + WTN + r % WTN;
-    } else {  // R3: X second halves
-      const int q = wave + 8 * (i - 4 - N2);
-      blk = (q / WTM) * 2 * WTM + WTM + q % WTM;
-    }
-    isx[i] = blk < BMP / 8;
-    dst[i] = blk * 1024;
-    const int row = 8 * blk + lr;
-    if (isx[i]) {
-      int xr = m0 + row;
-      if (xr >= M) xr = M - 1;  // rows past M: any valid row (never stored)
-      src[i] = (uint32_t)xr * K + 8 * (lc ^ lr);
-    } else {
-      src[i] = (uint32_t)(n0 + perm_row(row - BMP)) * K + 8 * (lc ^ lr);
-    }
-  }
-  auto dma = [&](int i, int kt) {
-    const hvk_bf16* s = (isx[i] ? X : Wt) + src[i] + kt * BK;
-    __builtin_amdgcn_global_load_lds((gbl_vptr_t)s, (lds_vptr_t)(smem + (kt & 1) * STAGE + dst[i]), 16, 0, 0);
-  };
-  auto dma_region = [&](int r, int kt) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-      if ((r == 1 && i < 4) || (r == 2 && i >= 4 && i < 4 + N2) || (r == 3 && i >= 4 + N2)) dma(i, kt);
-  };
-  // wait for the region of k-step tt: 8 DMAs of this wave are younger iff k-step tt+1 exists
-  auto wait_region = [&](int tt) {
-    if (tt + 1 < KT) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-
-  hvk_f32x4 acc[WTN][WTM];
-#pragma unroll
-  for (int a = 0; a < WTN; ++a)
-#pragma unroll
-    for (int b = 0; b < WTM; ++b) acc[a][b] = hvk_f32x4{0, 0, 0, 0};
-
-  // prologue: k-steps 0 and 1 (regions in order R1 R2 R3), wait for k-step 0
-#pragma unroll
-  for (int r = 1; r <= 3; ++r) dma_region(r, 0);
-  if (KT > 1) {
-#pragma unroll
-    for (int r = 1; r <= 3; ++r) dma_region(r, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-
-  hvk_u32x4 xf[HM][2], wf[WTN][2];
-  const uint32_t xrow = lds_u32(smem) + (16 * WTM * grp + li) * 128;
-  const uint32_t wrow = lds_u32(smem) + (BMP + 16 * WTN * wc + li) * 128;
-  const uint32_t sw0 = ((gq) ^ (li & 7)) << 4, sw1 = ((4 + gq) ^ (li & 7)) << 4;
-
-  for (int kt = 0; kt < KT; ++kt) {
-    const uint32_t sb = (kt & 1) * STAGE;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int hm = (p == 0 || p == 1) ? 0 : 1;  // quadrants (0,0) (0,1) (1,1) (1,0)
-      const int hn = (p == 0 || p == 3) ? 0 : 1;
-      // ---- memory part: this quadrant's new fragments, then the region waits / refills
-      if (p == 0 || p == 2) {
-#pragma unroll
-        for (int t = 0; t < HM; ++t) {
-          const uint32_t a = xrow + sb + (HM * hm + t) * 2048;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(xf[t][0]) : "v"(a + sw0));
-          asm volatile("ds_read_b128 %0, %1" : "=v"(xf[t][1]) : "v"(a + sw1));
-        }
-      }
-      if (p == 0 || p == 1) {
-#pragma unroll
-        for (int t = 0; t < HN; ++t) {
-          const uint32_t a = wrow + sb + (HN * hn + t) * 2048;
-          asm volatile("ds_read_b128 %0, %1" : "=v"(wf[HN * hn + t][0]) : "v"(a + sw0));
-          asm volatile("ds_read_b128 %0, %1" : "=v"(wf[HN * hn + t][1]) : "v"(a + sw1));
-        }
-      }
-      if (p == 0) {  // R2(kt) is read next phase; R3(kt+1) into the region phase 2 of kt-1 freed
-        wait_region(kt);
-        if (kt >= 1 && kt + 1 < KT) dma_region(3, kt + 1);
-      } else if (p == 1) {
-        wait_region(kt);  // R3(kt)
-      } else if (p == 2) {
-        if (kt + 2 < KT) dma_region(1, kt + 2);
-      } else {
-        wait_region(kt + 1);  // R1(kt+1)
-        if (kt + 2 < KT) dma_region(2, kt + 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- MFMA part
-      uint4 xa[HM][2], wa[HN][2];
-#pragma unroll
-      for (int t = 0; t < HM; ++t) { xa[t][0] = tie(xf[t][0]); xa[t][1] = tie(xf[t][1]); }
-#pragma unroll
-      for (int t = 0; t < HN; ++t) { wa[t][0] = tie(wf[HN * hn + t][0]); wa[t][1] = tie(wf[HN * hn + t][1]); }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int a = 0; a < HN; ++a)
-#pragma unroll
-          for (int b = 0; b < HM; ++b)
-            acc[HN * hn + a][HM * hm + b] = hvk_mfma16(wa[a][ks], xa[b][ks], acc[HN * hn + a][HM * hm + b]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();  // balance group 1's extra barrier
-
-  tile_epilogue<EPI, WTN, WTM, 0, HVK_TILE_STAGED ? BNP : 0, BMP, 512>(acc, bias, Y, Y2, M, N, m0 + 16 * WTM * grp,
-                                                                    n0 + 16 * WTN * wc, nullptr, nullptr, nullptr,
-                                                                    smem, m0, n0);
-}
-
 // algorithmic HBM bytes of one Y = X W^T launch: X, W read once, Y written once; EPI 1 also
 // writes GELU(h), EPI 2 reads h, EPI 4 writes 1/||.|| per token and q / k head (f32)
 double tile_bytes(int epi, double M, double N, double K) {
   return 2.0 * (M * K + N * K + M * N) + (epi == 1 || epi == 2 ? 2.0 * M * N : 0.0) +
          (epi == 4 ? 4.0 * M * (2.0 * N / 96.0) : 0.0) +
          (epi == 5 ? 10.0 * M * N + 8.0 * M : 0.0);  // EPI 5: x0 in, x + xb out, mean / rstd (x0 counted)
-}
-
-template <int EPI, int WTM, int WTN>
-int launch_pp_(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2,
-               int M, int N, int K, hipStream_t st) {
-  constexpr int BMP = 32 * WTM, BNP = 64 * WTN, LDS = 2 * (BMP + BNP) * 128;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<EPI, WTM, WTN>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  const int mtiles = (M + BMP - 1) / BMP;
-  const dim3 grid((mtiles + 7) / 8 * 8 * (N / BNP));
-  hvk_timer_shape("gemm_pp", EPI, BNP, M, N, K, tile_bytes(EPI, M, N, K));
-  HVK_LAUNCH_TIMED_W(HVK_TIMER_GEMM, 2.0 * M * N * K, (gemm_pp_kernel<EPI, WTM, WTN>), grid, dim3(512),
-                     LDS, st, X, W, bias, Y, Y2, M, N, K, mtiles);
-  HVK_CHECK_LAUNCH("hvk_gemm_tile(pp)");
-  return HVK_OK;
-}
-
-// ping-pong tile choice: 0 (default) off, 1 wherever a ping-pong tile divides N, 2 only
-// 256 x 256, 3 only 128 x 384; option "gemm_pp" (hvk_set_option / hvk_gemm_set_pp
-// (A/B runs and the tests that pin both kernels to the same bits).  Off by default: measured
-// 3-25 % slower than the 128-row tiles on every SwinV2 stage 1-3 shape (tools/bench_pp.py)
-static int gemm_pp_mode() { return (int)hvk_opt(HVK_OPT_GEMM_PP); }
-
-template <int EPI>
-int launch_pp(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf16* Y, hvk_bf16* Y2, int M,
-              int N, int K, hipStream_t st) {
-  const int mode = gemm_pp_mode();
-  // element offsets are 32-bit in the kernel
-  if (mode == 0 || (size_t)M * K >= (1u << 31) || (size_t)N * K >= (1u << 31)) return -1;
-  if (N % 256 == 0 && mode != 3) return launch_pp_<EPI, 8, 4>(X, W, bias, Y, Y2, M, N, K, st);
-  if (N % 384 == 0 && mode != 2) return launch_pp_<EPI, 4, 6>(X, W, bias, Y, Y2, M, N, K, st);
-  return -1;
 }
 
 template <int EPI, bool PIPE, int TN, int MG = 0>
@@ -824,23 +605,11 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   // input gradient, K = 1152: profiles/round4/tile_width_staged/); option "tile_wide" 0 / 1
   // forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
-  if (hvk_opt(HVK_OPT_GEMM_WIDE)) {  // the 208 x 384 whole-row tile where built
-    const int r = hvk_wide::launch(EPI, X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
-    if (r >= 0) return r;
-  }
   if constexpr (EPI == 4) {  // the qkv form: the 128-row tile kernel only
     if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1152)))
       return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
   } else {
-  {
-    const int r = launch_pp<EPI>(X, W, bias, Y, Y2, M, N, K, st);
-    if (r >= 0) return r;
-  }
-  if (hvk_opt(HVK_OPT_GEMM_XR)) {  // the persistent row-range kernel where it has a plan
-    const int r = hvk_xr::launch(EPI, X, W, bias, Y, Y2, M, N, K, st);
-    if (r >= 0) return r;
-  }
   // the fused fc1 + GELU epilogue (EPI 1) at K >= 384 (stages 2-3) prefers 128-column tiles:
   // half the per-tile epilogue, which the co-resident workgroup then hides better
   // (tools/gpu_tilew.sh: 2-7 % on s2/s3 fc1; 192 stays faster for stage-1 fc1 and for EPI 2)
@@ -889,13 +658,6 @@ int hvk_gemm_probe_read(void* dst, int nblocks) {
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
-
-int hvk_gemm_set_pp(int mode) {
-  if (mode < 0 || mode > 3) return hvk_set_error(HVK_EINVAL, "hvk_gemm_set_pp: mode %d not in 0..3", mode);
-  long long prev = 0;
-  hvk_set_option("gemm_pp", mode, &prev);
-  return (int)prev;
-}
 
 int hvk_gemm_supported(int M, int K, int N) {
   return M > 0 && K >= BK && K % BK == 0 && (N % TileCfg<4>::BN == 0 || N % TileCfg<6>::BN == 0) &&

@@ -29,11 +29,8 @@ enum HvkOption {
   HVK_OPT_WMSA_FWD_FORM = 0,    // w <= 8 forward: 0 one workgroup per (window, head group), 1 ring
   HVK_OPT_WMSA_BWD_NT,          // w <= 8 backward qkv reads: 0 cached, 1 nontemporal, 2 nt past 256 MB
   HVK_OPT_WMSA_BWD_SLICE_BYTES, // w <= 8 backward: batch slice so one launch's qkv stays below this
-  HVK_OPT_GEMM_PP,              // tiled GEMM: 0 128-row tiles, 1 ping-pong 256x256 / 128x384, 2 / 3 one of them
   HVK_OPT_TILE_WIDE,            // tiled GEMM: -1 by shape, 0 128-column, 1 192-column tiles
   HVK_OPT_DW_TILE,              // weight gradient, 192-multiple shapes: tile variant 4..8
-  HVK_OPT_GEMM_XR,              // tiled GEMM: persistent row-range kernel where it fits (1, 2: DMA interleaved), 0 off
-  HVK_OPT_GEMM_WIDE,            // tiled GEMM: 1 the 208 x 384 whole-row tile where built (gemm_wide.hip), 0 off
   HVK_OPT_WMSA_FWD_HG,          // w <= 8 forward (win form): heads per workgroup, 0 by head count, else 1 / 2 / 3 / 4 / 6
   HVK_OPT_DW_CHUNKS,            // weight gradient: workgroup target per launch (token chunks = target / output tiles)
   HVK_OPT_COUNT

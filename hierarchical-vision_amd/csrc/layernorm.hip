@@ -18,6 +18,7 @@
 // apart, each f32 instruction touching every line it read or wrote by halves -- 1.8x slower
 // at stage 0, tools/probe/ln_probe.hip, profiles/round4/ln_probe.txt.)  A wave works on 64/TPR
 // rows at once, grid-strided.  Row statistics are TPR-lane xor-shuffle reductions.
+#include <mutex>
 #include "hvk_common.h"
 
 #ifndef HVK_LN_X0_EARLY  // A/B build switch: residual loads issued with the branch-output loads
@@ -496,6 +497,18 @@ int hvk_ln_residual_bwd_split(const void* a, const float* abias, const float* ga
                          dgamma, dbeta, dabias, workspace, workspace_bytes, stream, param_stream);
 }
 
+// The ordering event of hvk_ln_residual_bwd_split, one per device (an event recorded on another
+// device's stream is invalid), created once under a lock (callers may be several host threads).
+static hipEvent_t split_event() {
+  static std::mutex mu;
+  static hipEvent_t ev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) ev[dev] = nullptr;
+  return ev[dev];
+}
+
 static int ln_residual_bwd(const void* a, const float* abias, const float* gamma, const float* sample_scale,
                            const float* mean, const float* rstd, const float* gx, const void* gxb, int rows, int C,
                            int rows_per_sample, float* gx0, void* ga, float* dgamma, float* dbeta, float* dabias,
@@ -520,9 +533,8 @@ static int ln_residual_bwd(const void* a, const float* abias, const float* gamma
   if (param_stream && param_stream != stream) {
     // the column sums (parameter gradients only) on the caller's parameter-gradient stream,
     // ordered after the row kernel by an event: they overlap the next input-gradient launches
-    static hipEvent_t ev = nullptr;
-    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-      return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd_split: event create failed");
+    hipEvent_t ev = split_event();
+    if (!ev) return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd_split: event create failed");
     cs = static_cast<hipStream_t>(param_stream);
     if (hipEventRecord(ev, st) != hipSuccess || hipStreamWaitEvent(cs, ev, 0) != hipSuccess)
       return hvk_set_error(HVK_EINVAL, "hvk_ln_residual_bwd_split: stream ordering failed");

@@ -628,8 +628,15 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   const unsigned long long st_loop_end = __builtin_amdgcn_s_memtime();
 #endif
 
-  // ---- workgroup reduction of the bias / scale gradients (carried as scale*dS), then one
-  // atomic per entry
+  // ---- the bias / scale / q_bias gradients of this (chunk, head), deterministically: the
+  // accumulator-order partials (carried as scale*dS) of the two pairs staged in LDS, folded into
+  // the (2w-1)^2 bins by one thread per bin in a fixed (query, key) order, the wave sums of d scale
+  // and d q_bias added in wave order, and the results added to this workgroup's own workspace slot
+  // (plain load + store: a later batch slice's launch adds in stream order); the finalize kernel
+  // sums the slots in chunk order.  No float atomics, so two runs give the same bits.
+  static_assert(kThreads == 256, "four waves: two pairs");
+  constexpr int RB = K::R * K::R, SLOT = bwd_slot_floats(WIN);
+  static_assert(RB <= kThreads, "one bin per thread");
   __syncthreads();
   const float inv_scale = 1.f / scale;
   float* red = reinterpret_cast<float*>(img0) + pair * (PC::PAIR_LDS / 2);  // pair p's images
@@ -644,21 +651,47 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   }
   __syncthreads();
   const float* red0 = reinterpret_cast<const float*>(img0);
-  float* dst = a.dbias_acc + (size_t)h * K::TAB;
-#if HVK_BWD_PROBE != 1  // timing probe: without the CPB-gradient atomics (results wrong)
-  for (int e = threadIdx.x; e < K::TAB; e += kThreads)
-    atomicAdd(dst + e, (red0[e] + red0[PC::PAIR_LDS / 2 + e]) * inv_scale);
-#endif
+  const int tid = threadIdx.x;
+  float binv = 0.f;
+  if (tid < RB) {  // bin (dy, dx) = (q_y - k_y, q_x - k_x) + (w - 1)
+    const int dy = tid / K::R - (WIN - 1), dx = tid % K::R - (WIN - 1);
+    const int y0 = dy > 0 ? dy : 0, y1 = dy < 0 ? WIN + dy : WIN;
+    const int x0 = dx > 0 ? dx : 0, x1 = dx < 0 ? WIN + dx : WIN;
+    for (int qy = y0; qy < y1; ++qy)
+      for (int qx = x0; qx < x1; ++qx) {
+        const int q = qy * WIN + qx, key = (qy - dy) * WIN + (qx - dx);
+        const int e = ((q >> 4) * NT + (key >> 4)) * 256 + ((q & 15) + 16 * ((key & 15) >> 2)) * 4 + (key & 3);
+        binv += red0[e] + red0[PC::PAIR_LDS / 2 + e];
+      }
+  }
   dscale = hvk_wave_sum(dscale);
-  // NORMED: the products summed were dS (sc2 cos)
-  if (lane == 0) atomicAdd(a.dscale_acc + h, NORMED ? dscale * inv_scale * inv_sc2 : dscale * inv_scale);
+  float qbv[2][4];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = hvk_row16_sum(dqb[dt][r]);
-      if (li == 0) atomicAdd(a.dqb_acc + h * 32 + 16 * dt + 4 * gq + r, v);
+    for (int r = 0; r < 4; ++r) qbv[dt][r] = hvk_row16_sum(dqb[dt][r]);
+  __syncthreads();  // the bin reads are done: stage the wave sums over the partials
+  float* stg = reinterpret_cast<float*>(img0);
+  // NORMED: the products summed were dS (sc2 cos)
+  if (lane == 0) stg[wave] = NORMED ? dscale * inv_scale * inv_sc2 : dscale * inv_scale;
+  if (li == 0) {
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[8 + wave * 32 + 16 * dt + 4 * gq + r] = qbv[dt][r];
+  }
+  __syncthreads();
+  float* slot = a.dbias_acc + ((size_t)h * a.slot_stride + chunk) * SLOT;
+  for (int i = tid; i < SLOT; i += kThreads) {
+    float v;
+    if (i < RB) v = binv * inv_scale;
+    else if (i == RB) v = (stg[0] + stg[1]) + (stg[2] + stg[3]);
+    else {
+      const int c = i - RB - 1;
+      v = (stg[8 + c] + stg[40 + c]) + (stg[72 + c] + stg[104 + c]);
     }
+    slot[i] += v;
+  }
 #ifdef HVK_STAMPS
   __syncthreads();
   if (lane == 0) {
@@ -668,31 +701,13 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 #endif
 }
 
-// Fold the accumulator-order partial sums into the CPB-table gradient [nH, R*R], write
-// dscale / dq_bias, and leave the workspace zero for the next call.
+// Sum the (head, chunk) slots in chunk order into the CPB-table gradient [nH, R*R], d scale and
+// d q_bias, and leave the workspace zero for the next call.
 template <int WIN>
 __global__ __launch_bounds__(256) void wmsa_finalize_kernel(BwdArgs a, float* __restrict__ dtab,
                                                             float* __restrict__ dscale,
                                                             float* __restrict__ dqb) {
-  using K = WinCfg<WIN>;
-  const int h = blockIdx.x;
-  float* acc = a.dbias_acc + (size_t)h * K::TAB;
-  __shared__ float bins[K::R * K::R];
-  for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) bins[i] = 0.f;
-  __syncthreads();
-  for (int e = threadIdx.x; e < K::TAB; e += blockDim.x) {
-    const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
-    const int qi = blk / K::NT, ki = blk % K::NT;
-    const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
-    if (q < K::N && key < K::N) {
-      const int idx = (q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1);
-      atomicAdd(&bins[idx], acc[e]);
-    }
-    acc[e] = 0.f;
-  }
-  finalize_scale_qb(a.dscale_acc, a.dqb_acc, dscale, dqb, h);
-  __syncthreads();
-  for (int i = threadIdx.x; i < K::R * K::R; i += blockDim.x) dtab[(size_t)h * K::R * K::R + i] = bins[i];
+  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x);
 }
 
 template <int WIN>
@@ -763,15 +778,10 @@ int hvk_debug_bwd_stamps(unsigned long long* out) {
 #endif
 
 size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window) {
-  // [dbias accumulators][dscale nH][dq_bias 32 nH] floats
-  size_t acc;
-  if (hvk_wmsa::large_window(window)) {
-    acc = hvk_wmsa::large_acc_floats(num_heads, window);
-  } else {
-    const int n = window * window, nt = (n + 15) / 16;
-    acc = (size_t)num_heads * nt * nt * 256;
-  }
-  return (acc + (size_t)num_heads * 33) * sizeof(float);
+  // [nH][slots per head][R*R bins, d scale, 32 d q_bias] floats (wmsa_common.h BwdArgs)
+  if (num_heads <= 0 || window <= 0) return 0;
+  return (size_t)num_heads * hvk_wmsa::bwd_slot_stride(num_heads, hvk_wmsa::large_window(window)) *
+         hvk_wmsa::bwd_slot_floats(window) * sizeof(float);
 }
 
 }  // extern "C"
@@ -833,11 +843,8 @@ int wmsa_bwd(const void* qkv, const float* rn, const void* dout, const void* out
   a.lse = lse;
   a.bias = bias_table;
   a.scale = scale;
-  const size_t ws_acc = hvk_wmsa_bwd_workspace_bytes(num_heads, window) / sizeof(float) -
-                        (size_t)num_heads * 33;
   a.dbias_acc = workspace;
-  a.dscale_acc = workspace + ws_acc;
-  a.dqb_acc = a.dscale_acc + num_heads;
+  a.slot_stride = hvk_wmsa::bwd_slot_stride(num_heads, hvk_wmsa::large_window(window));
   // one resident 4-wave workgroup per CU (128 KB LDS, 1 wave/SIMD)
   int rc = make_geom(B, H, W, C, num_heads, window, shift, 256, a.g);
   if (rc) return rc;

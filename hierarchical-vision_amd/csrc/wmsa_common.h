@@ -176,11 +176,13 @@ struct BwdArgs {
   hvk_bf16* dqkv;            // [T, 3C]
   const float* bias;         // [nH, R*R]
   const float* scale;        // [nH]
-  // workspace (zero on entry, re-zeroed by the finalize kernel):
-  float* dbias_acc;          // windows <= 8: [nH, TAB] accumulator-order partial sums;
-                             // large windows: [nH, R*R] bins
-  float* dscale_acc;         // [nH]
-  float* dqb_acc;            // [C]   column sums of dq (q_bias gradient)
+  // workspace (zero on entry, re-zeroed by the finalize kernel): one slot of
+  // bwd_slot_floats(win) = R*R CPB-table bins + d scale + 32 d q_bias per (head, chunk), written by
+  // the workgroup that owns (chunk, head) -- its partial sums folded in a fixed order, added to the
+  // slot without atomics -- and summed over chunks in chunk order by the finalize kernel, so
+  // every parameter gradient is deterministic (no float atomics in any order)
+  float* dbias_acc;          // [nH][slot_stride][bwd_slot_floats(win)]
+  int slot_stride;           // slots per head (>= n_chunks of every launch over this workspace)
   const float* rn;           // [T, 2nH] 1/max(||q||, eps), 1/max(||k||, eps) when q and k arrive
                              // normalised, q as q^ * scale * log2e (windows <= 8); null: raw q, k
   WmsaGeom g;
@@ -211,7 +213,6 @@ inline int make_geom(int B, int H, int W, int C, int nH, int win, int shift, int
 // large-window path (wmsa_large.hip): one workgroup per (window, head)
 bool large_window(int win);
 int large_fwd(const FwdArgs& a, int win, hipStream_t st);
-size_t large_acc_floats(int num_heads, int win);  // dbias_acc floats (bins)
 // backward + finalize: dbias_table [nH, R*R], dscale [nH], dq_bias [C] (may be null)
 int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,
               hipStream_t st);
@@ -223,17 +224,35 @@ int ring_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift,
 // burst per window, output rows stored from LDS
 int win_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, hipStream_t st);
 
-// finalize helper: per head block, write dscale / dq_bias from the workspace and zero it
-__device__ __forceinline__ void finalize_scale_qb(float* dscale_acc, float* dqb_acc, float* dscale,
-                                                  float* dqb, int h) {
-  if (threadIdx.x < 32) {
-    const int c = h * 32 + threadIdx.x;
-    if (dqb) dqb[c] = dqb_acc[c];
-    dqb_acc[c] = 0.f;
+// backward workspace: per (head, chunk) slot, R*R bins then d scale then 32 d q_bias
+__host__ __device__ constexpr int bwd_slot_floats(int win) { return (2 * win - 1) * (2 * win - 1) + 33; }
+// slots per head: the most chunks a launch over nH heads uses (wmsa_bwd: 512 / nH for windows
+// <= 8, make_geom's 256-workgroup plan for the large windows)
+inline int bwd_slot_stride(int num_heads, bool large) {
+  if (num_heads <= 0) return 1;
+  if (large) {
+    const int c = 256 / num_heads / 8 * 8;
+    return c < 8 ? 8 : c;
   }
-  if (threadIdx.x == 32) {
-    dscale[h] = dscale_acc[h];
-    dscale_acc[h] = 0.f;
+  const int c = 512 / num_heads;
+  return c < 1 ? 1 : c;
+}
+
+// finalize (one block per head): sum the head's slots in chunk order into the CPB-table gradient
+// [nH, R*R], d scale [nH] and d q_bias [C] (may be null), and leave the slots zero
+template <int WIN>
+__device__ __forceinline__ void finalize_slots(const BwdArgs& a, float* dtab, float* dscale, float* dqb, int h) {
+  constexpr int RR = (2 * WIN - 1) * (2 * WIN - 1), SLOT = bwd_slot_floats(WIN);
+  float* base = a.dbias_acc + (size_t)h * a.slot_stride * SLOT;
+  for (int i = threadIdx.x; i < SLOT; i += blockDim.x) {
+    float v = 0.f;
+    for (int c = 0; c < a.slot_stride; ++c) {
+      v += base[(size_t)c * SLOT + i];
+      base[(size_t)c * SLOT + i] = 0.f;
+    }
+    if (i < RR) dtab[(size_t)h * RR + i] = v;
+    else if (i == RR) dscale[h] = v;
+    else if (dqb) dqb[h * 32 + i - RR - 1] = v;
   }
 }
 

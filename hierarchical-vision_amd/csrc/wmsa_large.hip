@@ -989,35 +989,42 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     }
   }
 
-  float* gbias = a.dbias_acc + (size_t)h * K::RR;
+  // this (chunk, head)'s gradients, deterministically: the waves' private bins summed in wave
+  // order, the wave sums of d scale / d q_bias staged in LDS and added in wave order, all added to
+  // the workgroup's own workspace slot (no float atomics; the finalize sums slots in chunk order)
+  constexpr int SLOT = bwd_slot_floats(WIN);
+  float* slot = a.dbias_acc + ((size_t)h * a.slot_stride + chunk) * SLOT;
   for (int e = threadIdx.x; e < K::RR; e += 64 * F::WAVES) {
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < F::WAVES; ++c) v += bins[c * F::RRP + e];
-    atomicAdd(gbias + e, v);
+    slot[e] += v;
   }
   dscale = hvk_wave_sum(dscale);
-  if (lane == 0) atomicAdd(a.dscale_acc + h, dscale / sc2);
+  float qbv[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float v = hvk_row16_sum(dqb[e]);
-    if (li == 0) atomicAdd(a.dqb_acc + h * 32 + pcol + e, v);
+  for (int e = 0; e < 8; ++e) qbv[e] = hvk_row16_sum(dqb[e]);
+  float* stg = reinterpret_cast<float*>(img0);  // free: the last window's phase-2 reads are done
+  static_assert(F::WAVES <= 16, "stage layout");
+  if (lane == 0) stg[wave] = dscale / sc2;
+  if (li == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) stg[16 + wave * 32 + pcol + e] = qbv[e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 33) {
+    float v = 0.f;
+    for (int w = 0; w < F::WAVES; ++w) v += threadIdx.x == 0 ? stg[w] : stg[16 + w * 32 + threadIdx.x - 1];
+    slot[K::RR + threadIdx.x] += v;
   }
 }
 
-// copy the bins out, write dscale / dq_bias, leave the workspace zero
+// sum the (head, chunk) slots in chunk order into dtab / dscale / dq_bias, leave the workspace zero
 template <int WIN>
 __global__ __launch_bounds__(256) void wmsa_finalize_large_kernel(BwdArgs a, float* __restrict__ dtab,
                                                                   float* __restrict__ dscale,
                                                                   float* __restrict__ dqb) {
-  using K = LCfg<WIN>;
-  const int h = blockIdx.x;
-  float* acc = a.dbias_acc + (size_t)h * K::RR;
-  for (int i = threadIdx.x; i < K::RR; i += blockDim.x) {
-    dtab[(size_t)h * K::RR + i] = acc[i];
-    acc[i] = 0.f;
-  }
-  finalize_scale_qb(a.dscale_acc, a.dqb_acc, dscale, dqb, h);
+  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x);
 }
 
 template <int WIN, bool LSE>
@@ -1080,11 +1087,6 @@ int large_fwd(const FwdArgs& a, int win, hipStream_t st) {
     case 24: return launch_fwd_large<24>(a, st);
     default: return hvk_set_error(HVK_EUNSUPPORTED, "wmsa: window %d not built", win);
   }
-}
-
-size_t large_acc_floats(int num_heads, int win) {
-  const size_t r = 2 * (size_t)win - 1;
-  return (size_t)num_heads * r * r;
 }
 
 int large_bwd(const BwdArgs& a, int win, float* dbias_table, float* dscale, float* dq_bias,

@@ -49,8 +49,8 @@ class GradientBuckets:
         # grad_accum: microbatches before the last only accumulate into the bucket views (no
         # arrival count, no all-reduce: composer's DDP no_sync)
         self.accumulating = False
-        # measurement only (tools/ddp_trace.py): a list -> each bucket's all-reduce enqueue is
-        # marked by a timing event on the producing stream, (bucket, event) appended
+        # measurement only (Trainer.comm_timing, tools/ddp_trace.py): a list -> each bucket's
+        # all-reduce enqueue is marked on the producing stream, (bucket, trainer._Mark) appended
         self.trace = None
         self.buckets = []
         self._hooks = []
@@ -141,10 +141,9 @@ class GradientBuckets:
         self._pending[bi] -= 1
         if self._pending[bi] == 0 and self.enabled and not self.defer:
             flat = self.buckets[bi][0]
-            if self.trace is not None:
-                ev = torch.cuda.Event(enable_timing=True)
-                ev.record()
-                self.trace.append((bi, ev))
+            if self.trace is not None:  # the enqueue point on the producing stream (trainer._Mark)
+                from .trainer import _Mark
+                self.trace.append((bi, _Mark(p.is_cuda)))
             self._works[bi] = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg,
                                               async_op=True)
 

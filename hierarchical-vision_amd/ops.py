@@ -6,7 +6,6 @@ eager/CPU fallback: a CPU tensor or a missing library raises.
 """
 import contextlib
 import ctypes
-import weakref
 
 import torch
 import torch.nn.functional as F
@@ -179,7 +178,42 @@ class _WgradStream:
     active = False
     pending = False
     armed = False
-    produced = weakref.WeakSet()  # gradients written on the side stream (GradientBuckets' hooks)
+    produced = set()  # storage addresses of gradients written on the side stream (until the join)
+    uses = {}  # id(parameter) -> forward uses since the last backward join (note_leaf_uses)
+    forks = 0  # launches put on the side stream (wgrad_fork_count)
+
+
+def wgrad_fork_count():
+    """Parameter-gradient launches placed on the side stream since the process started."""
+    return _WgradStream.forks
+
+
+def note_leaf_uses(leaves, ctx):
+    """Count a forward use of each parameter in `leaves` (called by every Function's forward that
+    takes parameters; ctx: its context).  A parameter used twice in one graph (tied weights, a
+    module called twice) gets two gradients that autograd adds on the current stream, reading
+    side-written data without a wait: _wgrad_fork refuses it.  Forwards that build no graph (under
+    no_grad: grad mode is off inside every Function.forward, and needs_input_grad follows
+    requires_grad only) count as well, which errs on the safe side: until the next reset
+    (Trainer, each microbatch) or scope exit such a parameter stays on the current stream."""
+    if not (OPTIONS.wgrad_stream and any(ctx.needs_input_grad)):
+        return
+    for t in leaves:
+        if t is not None and t.requires_grad:
+            _WgradStream.uses[id(t)] = _WgradStream.uses.get(id(t), 0) + 1
+
+
+def _flat(leaves):
+    """((a, b), (c,)) -> (a, b, c)."""
+    out = []
+    for t in leaves:
+        out.extend(_flat(t) if isinstance(t, tuple) else (t,))
+    return tuple(out)
+
+
+def reset_leaf_uses():
+    """Forget the forward-use counts (the Trainer calls it before each microbatch's forward)."""
+    _WgradStream.uses.clear()
 
 
 @contextlib.contextmanager
@@ -197,6 +231,17 @@ def wgrad_stream_scope(enabled=True):
     finally:
         _WgradStream.active = prev
         join_wgrad()
+        _WgradStream.uses.clear()
+
+
+def _side_safe(t):
+    """A parameter whose fresh gradient autograd steals without touching it on the current
+    stream: a leaf with no gradient yet, f32 (no cast in validate_outputs), contiguous
+    (AccumulateGrad steals instead of cloning), no tensor hooks (register_hook runs on the
+    current stream; post-accumulate hooks -- GradientBuckets' -- handle the side stream
+    themselves) and exactly one forward use since the last join (no autograd-side sum)."""
+    return (t.is_leaf and t.grad is None and t.dtype == torch.float32 and t.is_contiguous()
+            and not t._backward_hooks and _WgradStream.uses.get(id(t), 0) == 1)
 
 
 def _wgrad_fork(leaves):
@@ -204,26 +249,28 @@ def _wgrad_fork(leaves):
     for) may be computed on the side stream, else None."""
     if not (OPTIONS.wgrad_stream and _WgradStream.active and leaves) or torch.cuda.is_current_stream_capturing():
         return None
-    if not all(t is None or (t.is_leaf and t.grad is None) for t in leaves):
+    if not all(t is None or _side_safe(t) for t in leaves):
         return None
     if _WgradStream.side is None:
         _WgradStream.side = torch.cuda.Stream()
     main = torch.cuda.current_stream()
     _WgradStream.side.wait_stream(main)
+    _WgradStream.forks += 1
     return main, _WgradStream.side
 
 
 def _wgrad_outputs(*ts):
-    """Mark gradients a side-stream launch wrote (wgrad_produced_on_side)."""
+    """Mark gradients a side-stream launch wrote (wgrad_produced_on_side), by storage address:
+    AccumulateGrad stores a detached alias (a new tensor object over the same storage)."""
     for t in ts:
         if t is not None:
-            _WgradStream.produced.add(t)
+            _WgradStream.produced.add(t.untyped_storage().data_ptr())
 
 
 def wgrad_produced_on_side(t):
-    """True for a gradient a side-stream launch wrote: a consumer on the side stream needs no
-    wait for the current stream to read it."""
-    return t in _WgradStream.produced
+    """True for a gradient a side-stream launch wrote (since the last join): a consumer on the
+    side stream needs no wait for the current stream to read it."""
+    return t is not None and t.untyped_storage().data_ptr() in _WgradStream.produced
 
 
 def _wgrad_joined(tensors):
@@ -254,6 +301,7 @@ def join_wgrad():
     if _WgradStream.pending:
         torch.cuda.current_stream().wait_stream(_WgradStream.side)
         _WgradStream.pending = False
+    _WgradStream.produced.clear()
 
 
 def wgrad_side_pending():
@@ -262,30 +310,72 @@ def wgrad_side_pending():
     return _WgradStream.side if _WgradStream.pending else None
 
 
+_DW_TOK = 32  # tokens per stage of libhvk's weight-gradient kernel (csrc/gemm_tn.hip TOK)
+
+
+def _dw_native(M, N, K, gelu_x=False):
+    """libhvk's weight-gradient kernel takes the shape: directly when 32 | M, else as a main launch
+    over the first M - M % 32 tokens plus one over the zero-padded 32-token tail (_dw_launch)."""
+    lib = _lib.load()
+    ok = lib.hvk_weight_grad_gelu_x_supported if gelu_x else lib.hvk_weight_grad_supported
+    return M > 0 and bool(ok(M - M % _DW_TOK if M >= _DW_TOK else _DW_TOK, N, K))
+
+
+def _dw_launch(g, x, with_db, gelu_x, xs, keep):
+    """(dW, db) from hvk_weight_grad / _gelu_x / _shift on the current stream; a ragged M (a
+    microbatch whose tokens are not a multiple of the kernel's 32-token stage) runs the aligned
+    part and the tail padded with zero rows (a zero g row adds nothing; GELU(0) = 0), summed.
+    Every tensor the launches touch is appended to `keep` (the side stream's record_stream)."""
+    lib = _lib.load()
+    M, N = g.shape
+    K = x.shape[1]
+    dev = g.device
+
+    def one(gg, xx):
+        m = gg.shape[0]
+        dw = torch.empty((N, K), device=dev, dtype=torch.float32)
+        db = torch.empty(N, device=dev, dtype=torch.float32) if with_db else None
+        nb = lib.hvk_weight_grad_workspace(m, N, K)
+        ws = torch.empty(nb // 4, device=dev, dtype=torch.float32)
+        if gelu_x:
+            call("hvk_weight_grad_gelu_x", ptr(gg), ptr(xx), ptr(dw), ptr(db), m, N, K, ptr(ws), nb, stream())
+        elif xs is not None:
+            call("hvk_weight_grad_shift", ptr(gg), ptr(xx), ptr(xs), ptr(dw), ptr(db), m, N, K, ptr(ws), nb, stream())
+        else:
+            call("hvk_weight_grad", ptr(gg), ptr(xx), ptr(dw), ptr(db), m, N, K, ptr(ws), nb, stream())
+        keep.extend((gg, xx, dw, db, ws))
+        return dw, db
+
+    tail = M % _DW_TOK
+    if not tail:
+        return one(g, x)
+    gt = torch.zeros((_DW_TOK, N), device=dev, dtype=g.dtype)
+    xt = torch.zeros((_DW_TOK, K), device=dev, dtype=x.dtype)
+    gt[:tail].copy_(g[M - tail:])
+    xt[:tail].copy_(x[M - tail:])
+    dw, db = one(gt, xt)
+    if M > tail:
+        dw0, db0 = one(g[:M - tail], x[:M - tail])
+        dw = dw0.add_(dw)
+        db = db0.add_(db) if with_db else None
+    return dw, db
+
+
 def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None, leaves=()):
     """weight_grad_sync, on the weight-gradient side stream when `leaves` (the parameters whose
     gradients dW / db are) allow it (wgrad_stream_scope) and libhvk's kernel is built for the
     shape, else on the current stream."""
-    lib = _lib.load()
     M, N = g.shape
     K = x.shape[1]
-    fork = _wgrad_fork(leaves) if g.is_cuda and (gelu_x or lib.hvk_weight_grad_supported(M, N, K)) else None
+    fork = _wgrad_fork(leaves) if g.is_cuda and _dw_native(M, N, K, gelu_x) else None
     if fork is None:
         return weight_grad_sync(g, x, with_db, gelu_x, xshift)
     main, side = fork
-    dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
-    db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
-    nb = lib.hvk_weight_grad_workspace(M, N, K)
-    ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
     xs = _f32(xshift) if xshift is not None else None
+    keep = [xs]
     with torch.cuda.stream(side):
-        if gelu_x:
-            call("hvk_weight_grad_gelu_x", ptr(g), ptr(x), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
-        elif xs is not None:
-            call("hvk_weight_grad_shift", ptr(g), ptr(x), ptr(xs), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
-        else:
-            call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db), M, N, K, ptr(ws), nb, stream())
-    _wgrad_joined((g, x, xs, dw, db, ws))
+        dw, db = _dw_launch(g, x, with_db, gelu_x, xs, keep)
+    _wgrad_joined(keep)
     _wgrad_outputs(dw, db)
     return dw, db
 
@@ -293,38 +383,20 @@ def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None, leaves=()):
 def weight_grad_sync(g, x, with_db=False, gelu_x=False, xshift=None):
     """(dW, db) = (g^T x, g.sum(0)) in f32 for g [M, N], x [M, K] bf16 with M = tokens (up to
     ~10^6): libhvk's token-chunked MFMA kernel with the bias gradient fused (hvk_weight_grad,
-    one pass over g) for every SwinV2-T shape it is built for; otherwise the library GEMM
-    batched over token chunks (thousands of workgroups) + a small sum.  db is None unless
-    with_db.  gelu_x: x holds the fc1 pre-activation h and the kernel contracts with GELU(h)
-    (hvk_weight_grad_gelu_x).  xshift (f32 [K]) or None: dW = g^T (x + 1 xshift^T)
-    (hvk_weight_grad_shift; the proj Linear's folded v_bias)."""
+    one pass over g) for every SwinV2 shape it is built for, any M (_dw_launch); otherwise the
+    library GEMM batched over token chunks + a small sum, counted as a library fallback.  db is
+    None unless with_db.  gelu_x: x holds the fc1 pre-activation h and the kernel contracts with
+    GELU(h) (hvk_weight_grad_gelu_x; callers check support).  xshift (f32 [K]) or None:
+    dW = g^T (x + 1 xshift^T) (hvk_weight_grad_shift; the proj Linear's folded v_bias)."""
     M, N = g.shape
     K = x.shape[1]
-    lib = _lib.load()
-    if gelu_x:  # x holds h; the kernel multiplies by GELU(h) (no fallback: callers check support)
-        dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
-        db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
-        nb = lib.hvk_weight_grad_workspace(M, N, K)
-        ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
-        call("hvk_weight_grad_gelu_x", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
-             ptr(ws), nb, stream())
-        return dw, db
-    if lib.hvk_weight_grad_supported(M, N, K):
-        dw = torch.empty((N, K), device=g.device, dtype=torch.float32)
-        db = torch.empty(N, device=g.device, dtype=torch.float32) if with_db else None
-        nb = lib.hvk_weight_grad_workspace(M, N, K)
-        ws = torch.empty(nb // 4, device=g.device, dtype=torch.float32)
-        if xshift is not None:
-            call("hvk_weight_grad_shift", ptr(g), ptr(x), ptr(_f32(xshift)), ptr(dw), ptr(db) if with_db else None,
-                 M, N, K, ptr(ws), nb, stream())
-        else:
-            call("hvk_weight_grad", ptr(g), ptr(x), ptr(dw), ptr(db) if with_db else None, M, N, K,
-                 ptr(ws), nb, stream())
-        return dw, db
+    if gelu_x or _dw_native(M, N, K):
+        return _dw_launch(g, x, with_db, gelu_x, _f32(xshift) if xshift is not None else None, [])
     if xshift is not None:
         dw, db = weight_grad(g, x, True)
         dw.add_(torch.outer(db, _f32(xshift)))
         return dw, (db if with_db else None)
+    library_fallback("weight_grad", f"M={M} N={N} K={K}")
     db = g.sum(dim=0, dtype=torch.float32) if with_db else None
     nc = _split_k_chunks(M)
     if nc == 1:
@@ -335,7 +407,38 @@ def weight_grad_sync(g, x, with_db=False, gelu_x=False, xshift=None):
     return part.sum(dim=0), db
 
 
+LIBRARY_FALLBACKS = {}  # site -> launches that left libhvk for a torch / hipBLASLt op
+
+
+def library_fallback(site, detail=""):
+    """Record a product-path launch that leaves libhvk (a shape no hand-written kernel is built
+    for); with options.strict_native it raises instead.  bench.py prints the counts and the
+    bench-routing tests assert they stay zero."""
+    if OPTIONS.strict_native:
+        raise RuntimeError(f"library fallback at {site} {detail} (options.strict_native)")
+    LIBRARY_FALLBACKS[site] = LIBRARY_FALLBACKS.get(site, 0) + 1
+
+
+def library_fallbacks(reset=False):
+    """{site: count} of library fallbacks since the last reset."""
+    out = dict(LIBRARY_FALLBACKS)
+    if reset:
+        LIBRARY_FALLBACKS.clear()
+    return out
+
+
 _LIN_OK = {}
+_TILE_ANY = {}
+
+
+def _tile_any(M, K, N):
+    """libhvk's tiled GEMM takes the shape at all (hvk_gemm_supported: K % 64, 128 | N or 192 | N,
+    any M): the native route for shapes outside the measured speed rules of _tile_ok and the
+    skinny kernel's table (small microbatches), instead of the library GEMM."""
+    ok = _TILE_ANY.get((K, N))
+    if ok is None:
+        ok = _TILE_ANY[(K, N)] = bool(_lib.load().hvk_gemm_supported(1, K, N))
+    return ok and M > 0
 
 
 def _linear_native(M, K, N):
@@ -364,7 +467,14 @@ def _tile_ok(M, K, N):
 
 def _native_nt(M, K, N):
     """True when mm_nt runs one of libhvk's GEMMs for this shape."""
-    return _tile_ok(M, K, N) or _linear_native(M, K, N)
+    return _tile_ok(M, K, N) or _linear_native(M, K, N) or _tile_any(M, K, N)
+
+
+def _dgrad_fallback(g2, wb):
+    """Input gradient g2 wb for a shape no libhvk GEMM takes (counted / strict, see
+    library_fallback)."""
+    library_fallback("dgrad", f"M={g2.shape[0]} N={wb.shape[0]} K={wb.shape[1]}")
+    return g2 @ wb
 
 
 def _gelu_skinny_k():
@@ -381,7 +491,7 @@ def gelu_fwd(x2, wb, bias):
     lib = _lib.load()
     if (K in _gelu_skinny_k() or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N):
         fn = "hvk_linear_gelu_fwd"
-    elif _tile_ok(M, K, N):
+    elif _tile_any(M, K, N):
         fn = "hvk_gemm_gelu_fwd"
     else:
         return None
@@ -401,23 +511,24 @@ def _skinny_first(M, K, N):
 
 
 def mm_nt(x2, wb, bias=None):
-    """y = x2 wb^T (+ bias): libhvk's MFMA kernels where built (skinny weight-stationary for
-    the memory-bound stage 0-1 shapes, tiled for stage 2), else the library GEMM.  x2 [M, K]
+    """y = x2 wb^T (+ bias): libhvk's MFMA kernels -- skinny weight-stationary for the
+    memory-bound stage 0-1 shapes, tiled for stages 2-3 (and any other shape the tile takes:
+    small microbatches) -- else the library GEMM, counted as a library fallback.  x2 [M, K]
     bf16, wb [N, K] bf16, bias f32 [N]."""
     M, K = x2.shape
     N = wb.shape[0]
-    if _tile_ok(M, K, N) and not _skinny_first(M, K, N):
+    b = _f32(bias) if bias is not None else None
+    if (_tile_ok(M, K, N) and not _skinny_first(M, K, N)) or (not _linear_native(M, K, N) and _tile_any(M, K, N)):
         y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
-        b = _f32(bias) if bias is not None else None
         call("hvk_gemm_fwd", ptr(x2), ptr(wb), ptr(b) if b is not None else None, ptr(y), M, K, N,
              stream())
         return y
     if _linear_native(M, K, N):
         y = torch.empty((M, N), device=x2.device, dtype=torch.bfloat16)
-        b = _f32(bias) if bias is not None else None
         call("hvk_linear_fwd", ptr(x2), ptr(wb), ptr(b) if b is not None else None, ptr(y), M, K,
              N, stream())
         return y
+    library_fallback("mm_nt", f"M={M} K={K} N={N}")
     return F.linear(x2, wb, bias.to(torch.bfloat16) if bias is not None else None)
 
 
@@ -437,6 +548,7 @@ class LinearFn(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.xshift = xshift.detach() if xshift is not None else None
         ctx.leaves = (weight, bias)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         return y
 
     @staticmethod
@@ -447,12 +559,13 @@ class LinearFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K)
-                  else g2 @ wb).reshape(xb.shape)
+                  else _dgrad_fallback(g2, wb)).reshape(xb.shape)
         want_db = ctx.has_bias and ctx.needs_input_grad[2]
         dw, db = None, None
         if ctx.needs_input_grad[1]:
             dw, db = weight_grad(g2, xb.reshape(-1, K), want_db, xshift=getattr(ctx, "xshift", None),
-                                 leaves=ctx.leaves if want_db or not ctx.has_bias else ())
+                                 leaves=(ctx.leaves[0], ctx.leaves[1] if want_db else None)
+                                 if want_db or not ctx.has_bias or OPTIONS.wgrad_stream_qkv else ())
         elif want_db:
             db = g2.sum(dim=0, dtype=torch.float32)
         return gx, dw, db, None
@@ -478,9 +591,10 @@ def qkv_nt(x2, wb, bias, scale):
     rn = torch.empty((M, 2 * N // 96), device=x2.device, dtype=torch.float32)
     b = ptr(_f32(bias)) if bias is not None else None
     sc = _f32(scale.detach())  # its gradient comes from the attention core (logit = scale cos)
-    if _tile_ok(M, K, N) and not _skinny_first(M, K, N) and N % 96 == 0:
+    skinny = _linear_native(M, K, N) and lib.hvk_linear_qkv_supported(M, K, N)
+    if N % 96 == 0 and ((_tile_ok(M, K, N) and not _skinny_first(M, K, N)) or (not skinny and _tile_any(M, K, N))):
         call("hvk_gemm_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), ptr(sc), M, K, N, stream())
-    elif _linear_native(M, K, N) and lib.hvk_linear_qkv_supported(M, K, N):
+    elif skinny:
         call("hvk_linear_qkv_fwd", ptr(x2), ptr(wb), b, ptr(y), ptr(rn), ptr(sc), M, K, N, stream())
     else:
         y = mm_nt(x2, wb, bias)
@@ -504,6 +618,8 @@ class LinearQkvFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wb)
         ctx.wt = wt
         ctx.has_bias = bias is not None
+        ctx.leaves = (weight, bias)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         ctx.mark_non_differentiable(rn)
         ctx.set_materialize_grads(False)  # no zero-filled gradient for rn (one fill per block)
         return y.reshape(*xb.shape[:-1], N), rn
@@ -561,6 +677,7 @@ class HeadFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n_w, *wb):
+        note_leaf_uses(wb, ctx)
         ws, bs = wb[:n_w], wb[n_w:]
         xb = _bf16(x).contiguous()
         M, K = xb.shape
@@ -643,6 +760,7 @@ class AttnBiasFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, v_bias, proj_bias, proj_w, q_bias):
+        note_leaf_uses((v_bias, proj_bias, proj_w), ctx)
         C = v_bias.numel()
         v, w = _f32(v_bias), _f32(proj_w)
         pb = _f32(proj_bias) if proj_bias is not None else None
@@ -706,6 +824,7 @@ class WindowAttentionCore(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, q_bias, bias_table, scale, H, W, num_heads, window, shift, rn=None):
+        note_leaf_uses((q_bias,), ctx)
         B, L, C3 = qkv.shape
         C = C3 // 3
         if L != H * W:
@@ -792,6 +911,7 @@ class CpbTable(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, coords, w1, b1, w2, logit_scale, clamp_max):
+        note_leaf_uses((w1, b1, w2, logit_scale), ctx)
         coords, w1, b1, w2 = _f32(coords), _f32(w1), _f32(b1), _f32(w2)
         logit = _f32(logit_scale.reshape(-1))
         nH, hid = w2.shape
@@ -859,6 +979,7 @@ class BlockTables(torch.autograd.Function):
         ctx.clamp_max = float(clamp_max)
         ctx.logit_shape = logit_scale.shape
         ctx.leaves = (v_bias, proj_bias, proj_w, w1, b1, w2, logit_scale)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         ctx.mark_non_differentiable(qkv_bias)
         ctx.set_materialize_grads(False)
         return qkv_bias, eff, table, scale
@@ -929,6 +1050,7 @@ class LayerNormResidual(torch.autograd.Function):
              ptr(rstd), stream())
         ctx.save_for_backward(a, abias, gamma, sample_scale, mean, rstd)
         ctx.ln_leaves = (abias_p, gamma_p, beta_p)
+        note_leaf_uses(_flat(ctx.ln_leaves), ctx)
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
         # an unused output (e.g. the bf16 copy at a stage end) gets None, not a zero-filled
@@ -994,6 +1116,7 @@ class LinearLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, inp, weight, xshift, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
         ctx.ln_leaves = (abias, gamma, beta)
+        note_leaf_uses(_flat(ctx.ln_leaves), ctx)
         xin = _bf16(inp)
         wb, wt = _bf16_weight(weight)
         N, K = wb.shape
@@ -1010,6 +1133,7 @@ class LinearLNFn(torch.autograd.Function):
         ctx.save_for_backward(xin, wb, a, abias, gamma, sample_scale, mean, rstd)
         ctx.wt = wt
         ctx.leaves = (weight,)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         ctx.xshift = xshift.detach() if xshift is not None else None
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
@@ -1027,7 +1151,8 @@ class LinearLNFn(torch.autograd.Function):
         g2 = ga.reshape(-1, N)
         gin = None
         if ctx.needs_input_grad[0]:
-            gin = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K) else g2 @ wb).reshape(xin.shape)
+            gin = (mm_nt(g2, _bf16_t(wb, ctx.wt)) if _native_nt(g2.shape[0], N, K)
+                   else _dgrad_fallback(g2, wb)).reshape(xin.shape)
         dw = (weight_grad(g2, xin.reshape(-1, K), False, xshift=ctx.xshift, leaves=ctx.leaves)[0]
               if ctx.needs_input_grad[1] else None)
         return gin, dw, None, dabias, gx0, dgamma, dbeta, None, None, None
@@ -1059,6 +1184,7 @@ class NormPool(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, eps):
+        note_leaf_uses((gamma, beta), ctx)
         x = _f32(x)
         B, T, C = x.shape
         dev = x.device
@@ -1137,6 +1263,7 @@ class LinearGelu(torch.autograd.Function):
         ctx.save_for_backward(xb, wb, h)
         ctx.wt = wt
         ctx.leaves = (weight,)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         return y.reshape(*xb.shape[:-1], N)
 
     @staticmethod
@@ -1154,7 +1281,7 @@ class LinearGelu(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, _bf16_t(wb, ctx.wt)) if _native_nt(M, N, K)
-                  else gh @ wb).reshape(xb.shape)
+                  else _dgrad_fallback(gh, wb)).reshape(xb.shape)
         dw = weight_grad(gh, xb.reshape(-1, K), leaves=ctx.leaves)[0] if ctx.needs_input_grad[1] else None
         return gx, dw, db
 
@@ -1164,7 +1291,7 @@ def linear_gelu(x, weight, bias):
     N, K = weight.shape
     M = x.numel() // K
     if bias is not None and (((K in (96, 192) or K in _skinny_first_k())
-                              and _lib.load().hvk_linear_gelu_supported(M, K, N)) or _tile_ok(M, K, N)):
+                              and _lib.load().hvk_linear_gelu_supported(M, K, N)) or _tile_any(M, K, N)):
         return LinearGelu.apply(x, weight, bias)
     return bias_gelu(linear(x, weight), bias)
 
@@ -1210,6 +1337,7 @@ class MlpFn(torch.autograd.Function):
             ctx.save_for_backward(xb, w1b, w2b, h, y1)
         ctx.has_b2 = b2 is not None
         ctx.leaves = ((w1, b1), (w2, b2))
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         return y.reshape(*xb.shape[:-1], N2)
 
     @staticmethod
@@ -1237,8 +1365,9 @@ class MlpFn(torch.autograd.Function):
                  M, N2, N1, K, stream())
             dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=ctx.leaves[0])  # fc1 bias gradient fused
             return gx.reshape(xb.shape), dw1, db1, dw2, db2
-        if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
-                                         _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
+        lib = _lib.load()
+        if ((_tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and lib.hvk_linear_gelu_bwd_supported(M, N2, N1)))
+                or not lib.hvk_linear_gelu_bwd_supported(M, N2, N1)):
             call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
         else:
             call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1,
@@ -1246,7 +1375,7 @@ class MlpFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[0]:
             gx = (mm_nt(gh, _bf16_t(w1b, ctx.wts[0])) if _native_nt(M, N1, K)
-                  else gh @ w1b).reshape(xb.shape)
+                  else _dgrad_fallback(gh, w1b)).reshape(xb.shape)
         dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=ctx.leaves[0])  # fc1 bias gradient fused
         return gx, dw1, db1, dw2, db2
 
@@ -1262,6 +1391,7 @@ class MlpLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, inp, w1, b1, w2, abias, x0, gamma, beta, sample_scale, rows_per_sample, eps):
         ctx.ln_leaves = (abias, gamma, beta)
+        note_leaf_uses(_flat(ctx.ln_leaves), ctx)
         xin = _bf16(inp)
         w1b, w1t = _bf16_weight(w1)
         w2b, w2t = _bf16_weight(w2)
@@ -1289,6 +1419,7 @@ class MlpLNFn(torch.autograd.Function):
         ctx.save_for_backward(xin, w1b, w2b, h, y1, a, abias, gamma, sample_scale, mean, rstd)
         ctx.wts = (w1t, w2t)
         ctx.leaves = ((w1, b1), (w2,))
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         ctx.has_x0 = x0 is not None
         ctx.rps = rows_per_sample
         ctx.set_materialize_grads(False)
@@ -1339,14 +1470,16 @@ def _mlp_bwd_tiled(gy, xb, w1b, w2b, h, y1, wts, want_x, leaves=((), ())):
     dw2 = weight_grad(g2, y1, leaves=leaves[1])[0]
     gh = torch.empty_like(h)
     w2t = _bf16_t(w2b, wts[1])
-    if _tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and
-                                     _lib.load().hvk_linear_gelu_bwd_supported(M, N2, N1)):
+    lib = _lib.load()
+    if ((_tile_ok(M, N2, N1) and not (N2 in _skinny_first_k() and lib.hvk_linear_gelu_bwd_supported(M, N2, N1)))
+            or not lib.hvk_linear_gelu_bwd_supported(M, N2, N1)):
         call("hvk_gemm_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), M, N2, N1, stream())
     else:
         call("hvk_linear_gelu_bwd", ptr(g2), ptr(w2t), ptr(h), ptr(gh), None, M, N2, N1, stream())
     gx = None
     if want_x:
-        gx = (mm_nt(gh, _bf16_t(w1b, wts[0])) if _native_nt(M, N1, K) else gh @ w1b).reshape(xb.shape)
+        gx = (mm_nt(gh, _bf16_t(w1b, wts[0])) if _native_nt(M, N1, K)
+              else _dgrad_fallback(gh, w1b)).reshape(xb.shape)
     dw1, db1 = weight_grad(gh, xb.reshape(-1, K), True, leaves=leaves[0])  # fc1 bias gradient fused
     return gx, dw1, db1, dw2
 
@@ -1361,8 +1494,8 @@ def mlp_ln_supported(M, K, N1, N2):
         return True
     return (N2 != 96 and linear_ln_supported(M, N1, N2) and not _gelu_recompute(M, K, N1, N2)
             and (((K in _gelu_skinny_k() or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N1))
-                 or _tile_ok(M, K, N1))
-            and (lib.hvk_linear_gelu_bwd_supported(M, N2, N1) or _tile_ok(M, N2, N1)))
+                 or _tile_any(M, K, N1))
+            and (lib.hvk_linear_gelu_bwd_supported(M, N2, N1) or _tile_any(M, N2, N1)))
 
 
 def mlp_ln(x, w1, b1, w2, x0, gamma, beta, sample_scale=None, rows_per_sample=1, eps=1e-5, abias=None):
@@ -1378,8 +1511,8 @@ def mlp(x, w1, b1, w2, b2=None):
     M = x.numel() // K
     lib = _lib.load()
     if (b1 is not None and (((K in (96, 192) or K in _skinny_first_k()) and lib.hvk_linear_gelu_supported(M, K, N1))
-                            or _tile_ok(M, K, N1))
-            and (lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1) or _tile_ok(M, w2.shape[0], N1))):
+                            or _tile_any(M, K, N1))
+            and (lib.hvk_linear_gelu_bwd_supported(M, w2.shape[0], N1) or _tile_any(M, w2.shape[0], N1))):
         return MlpFn.apply(x, w1, b1, w2, b2)
     return linear(linear_gelu(x, w1, b1), w2, b2)
 
@@ -1506,6 +1639,7 @@ class MergeLinearFn(torch.autograd.Function):
         ctx.wt = wt
         ctx.geo = (B, H, W, C, N)
         ctx.leaves = (weight,)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         return y
 
     @staticmethod
@@ -1523,6 +1657,7 @@ class MergeLinearLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, eps, H, W):
         ctx.ln_leaves = (gamma, beta)
+        note_leaf_uses(_flat(ctx.ln_leaves), ctx)
         xb = _bf16(x).contiguous()
         wb, wt = _bf16_weight(weight)
         B, L, C = xb.shape
@@ -1537,6 +1672,7 @@ class MergeLinearLNFn(torch.autograd.Function):
         ctx.wt = wt
         ctx.geo = (B, H, W, C, N)
         ctx.leaves = (weight,)
+        note_leaf_uses(_flat(ctx.leaves), ctx)
         ctx.set_materialize_grads(False)
         return xo, xob
 

@@ -51,6 +51,13 @@ class HostOptions:
     # off, measured -1.5 % against the side stream without them (3 interleaved runs,
     # profiles/round5/wgrad_stream/ab_ln.txt)
     wgrad_stream_ln: bool = False
+    # ... including the qkv Linear's weight gradient (its bias gradient comes out of the W-MSA
+    # backward, so that Linear has no bias gradient of its own; round 5 left it on the main stream)
+    wgrad_stream_qkv: bool = True
+    # ... also at world > 1, where the bucket all-reduces then start from the side stream: off
+    # until RCCL over xGMI says otherwise (the dp2 gloo rehearsal measured -8 %); bench.py
+    # --host-opt wgrad_stream_multi_rank=1 is the 8-GPU A/B, its `comm` block the diagnosis
+    wgrad_stream_multi_rank: bool = False
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward
@@ -61,6 +68,10 @@ class HostOptions:
     s1_gelu_tile: bool = False
     # keep only fc1's h at stage 0 and recompute GELU(h) where consumed (measured -0.4 %)
     gelu_recompute: bool = False
+    # a product-path launch that would leave libhvk for a torch / hipBLASLt op (a shape no
+    # hand-written kernel takes) raises instead of being counted (ops.library_fallback); the
+    # bench-routing parity tests run with it on
+    strict_native: bool = False
 
 
 OPTIONS = HostOptions()

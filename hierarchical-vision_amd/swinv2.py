@@ -681,6 +681,8 @@ class SwinTransformerV2(nn.Module):
                 and _lib_ln_pool_ok(self.num_features)):
             y = ops.norm_pool(s.f32, self.norm.weight, self.norm.bias, self.norm.eps)  # one kernel
         else:
+            if s.f32.is_cuda:
+                ops.library_fallback("norm_pool", f"C={self.num_features}")
             with torch.autocast(device_type=x.device.type, enabled=False):
                 y = F.layer_norm(s.f32, (self.num_features,), self.norm.weight, self.norm.bias,
                                  self.norm.eps)

@@ -11,11 +11,14 @@ clipping + optimizer update as a second one; a step is two graph replays with, f
 world > 1, the bucketed RCCL all-reduce issued eagerly between them (RCCL is not captured).
 The batch must live in the static tensors passed to capture() (copy new data into them).
 BATCH_END algorithms (EMA: host-side counters) run eagerly after the replays."""
+import time
+
 import torch
 
 from . import ops
 from .algorithmic import Event, State
 from .ddp import GradientBuckets
+from .options import OPTIONS
 
 
 def resolve_grad_accum(grad_accum, device_type):
@@ -44,6 +47,45 @@ def _split_batch(batch, n):
             for i in range(n)]
 
 
+class _Mark:
+    """A point in the step's timeline: a timing event on the current HIP stream (CUDA), else the
+    host clock (CPU / gloo tests, where the backward runs synchronously)."""
+
+    def __init__(self, cuda):
+        if cuda:
+            self.ev = torch.cuda.Event(enable_timing=True)
+            self.ev.record()
+        else:
+            self.ev, self.t = None, time.perf_counter()
+
+    def ms_to(self, later):
+        if self.ev is not None:
+            return self.ev.elapsed_time(later.ev)
+        return 1000.0 * (later.t - self.t)
+
+
+def comm_report(records):
+    """Exchange timing of the steps recorded with Trainer.comm_timing = [] (world > 1):
+    exposed_ms = mean GPU time from the end of the backward to the point where the current stream
+    has waited for every bucket's all-reduce (buckets.synchronize(); the exchange time the
+    backward did not hide), backward_ms its mean length, and per bucket the mean enqueue offset
+    before the end of the backward (ms; the overlap window each all-reduce had).  Synchronises."""
+    if not records:
+        return None
+    if records[0]["bwd_start"].ev is not None:
+        torch.cuda.synchronize()
+    exposed = [r["bwd_end"].ms_to(r["sync_end"]) for r in records]
+    bwd = [r["bwd_start"].ms_to(r["bwd_end"]) for r in records]
+    nb = max(len(r["buckets"]) for r in records)
+    offs = [[] for _ in range(nb)]
+    for r in records:
+        for bi, e in r["buckets"]:
+            offs[bi].append(e.ms_to(r["bwd_end"]))
+    return {"steps": len(records), "exposed_ms": round(sum(exposed) / len(exposed), 3),
+            "exposed_ms_max": round(max(exposed), 3), "backward_ms": round(sum(bwd) / len(bwd), 3),
+            "bucket_enqueue_before_bwd_end_ms": [round(sum(o) / len(o), 3) if o else None for o in offs]}
+
+
 class Trainer:
     def __init__(self, model, optimizer, algorithms=(), bucket_mb=64.0, dtype=torch.bfloat16,
                  device_transforms=None, grad_accum=1):
@@ -62,6 +104,8 @@ class Trainer:
         self.buckets = GradientBuckets(model, bucket_mb=bucket_mb)
         dev = next(model.parameters()).device.type
         self.grad_accum = resolve_grad_accum(grad_accum, dev)
+        # a list -> each eager step appends its exchange timing events (comm_report); None: off
+        self.comm_timing = None
         self._run(Event.INIT)
 
     def _run(self, event):
@@ -87,6 +131,7 @@ class Trainer:
             # (DDP no_sync for the others)
             self.buckets.accumulating = i < len(micro) - 1
             st.batch = mb
+            ops.reset_leaf_uses()  # the side stream's per-parameter use counts start with this forward
             with torch.autocast(device_type=dev_type, dtype=self.dtype, enabled=dev_type == "cuda"):
                 st.outputs = self.model(st.batch)
             self._run(Event.BEFORE_LOSS)
@@ -96,16 +141,28 @@ class Trainer:
                 st.loss = st.loss * (1.0 / len(micro))
             # single rank: parameter gradients may run on the weight-gradient side stream
             # (ops.wgrad_stream_scope; a parameter still holding a gradient, i.e. a later
-            # microbatch, stays on this stream).  Not with the bucketed all-reduce: a bucket can
-            # only start once the side stream, which runs behind, has produced it (the dp2 gloo
-            # rehearsal measured -8 %, profiles/round5/wgrad_stream/dp2_ab.txt)
-            with ops.wgrad_stream_scope(dev_type == "cuda" and not self.buckets.enabled):
+            # microbatch, stays on this stream).  With the bucketed all-reduce only under
+            # options.wgrad_stream_multi_rank: a bucket can only start once the side stream, which
+            # runs behind, has produced it (the dp2 gloo rehearsal measured -8 %,
+            # profiles/round5/wgrad_stream/dp2_ab.txt; RCCL over xGMI is unmeasured)
+            side = dev_type == "cuda" and (not self.buckets.enabled or OPTIONS.wgrad_stream_multi_rank)
+            timing = self.comm_timing is not None and self.buckets.enabled and i == len(micro) - 1
+            if timing:
+                ev = {"bwd_start": _Mark(dev_type == "cuda")}
+                self.buckets.trace = []
+            with ops.wgrad_stream_scope(side):
                 st.loss.backward()
+            if timing:
+                ev["bwd_end"] = _Mark(dev_type == "cuda")
             total = st.loss.detach() if total is None else total + st.loss.detach()
         self.buckets.accumulating = False
         st.batch = batch
         st.loss = total
         self._grad_mean()
+        if timing:
+            ev["sync_end"] = _Mark(dev_type == "cuda")
+            ev["buckets"], self.buckets.trace = self.buckets.trace, None
+            self.comm_timing.append(ev)
         self._run(Event.AFTER_BACKWARD)
         self.optimizer.step()
         self.buckets.reset()

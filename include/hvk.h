@@ -23,7 +23,7 @@ extern "C" {
 #endif
 
 /* the C ABI this header describes; hvk_abi_version() returns it (bindings check it at load) */
-#define HVK_ABI_VERSION 13
+#define HVK_ABI_VERSION 14
 
 #define HVK_OK 0
 #define HVK_EINVAL 1
@@ -43,14 +43,8 @@ const char* hvk_last_error_string(void);
  *                         qkv exceeds the 256 MB Infinity Cache
  *   wmsa_bwd_slice_bytes  w <= 8 backward: launch over batch slices whose qkv stays below this
  *                         (default 2^31, the buffer-descriptor range)
- *   gemm_pp               tiled GEMM kernel choice (hvk_gemm_set_pp below), default 0
  *   tile_wide             tiled GEMM: -1 (default) tile width by shape, 0 128, 1 192 columns
  *   dw_tile               weight gradient at 192-multiple shapes: tile variant 4..8 (default 5)
- *   gemm_xr               tiled GEMM: 0 (default) tile kernel, 1 / 2 the persistent row-range
- *                         kernel (gemm_xr.hip; bit-identical, measured slower)
- *   gemm_wide             tiled GEMM (epilogues 0 / 1 / 2 / 4): 1 the 208 x 384 whole-row tile,
- *                         one 512-thread workgroup per CU (gemm_wide.hip; bit-identical) where
- *                         built (N % 384, K % 32, M >= 1664), 0 the 128-row tiles
  *   wmsa_fwd_hg           w <= 8 forward, win form: heads per workgroup; 0 (default) 2 at 6 heads,
  *                         else 3 where it divides the head count, else 2, else 1; 1 / 2 / 3 / 4 / 6
  *                         force it where it divides (the same results bit for bit: per-head math
@@ -114,7 +108,10 @@ size_t hvk_wmsa_bwd_workspace_bytes(int num_heads, int window);
  * replacing the qkv bias-gradient reduction) or NULL; dbias_table: f32 [num_heads,
  * (2w-1)^2] (overwritten); dscale: f32 [num_heads] (overwritten, d loss / d scale).
  * workspace: f32, hvk_wmsa_bwd_workspace_bytes bytes, ALL ZERO on entry and left all zero
- * on return (a caller keeps one zero-filled workspace: no memset per call). */
+ * on return (a caller keeps one zero-filled workspace: no memset per call).  It holds one slot
+ * (CPB-table bins, d scale, d q_bias) per (head, window chunk): each workgroup adds its partial
+ * sums, folded in a fixed order, to its own slot and the finalize kernel sums the slots in chunk
+ * order -- no float atomics, so dbias_table / dscale / dq_bias are bit-identical run to run. */
 int hvk_wmsa_bwd(const void* qkv, const void* dout, const void* out, const float* lse, void* dqkv,
                  float* dq_bias, const float* bias_table, const float* scale, float* dbias_table,
                  float* dscale, float* workspace, size_t workspace_bytes, int B, int H, int W, int C,
@@ -234,12 +231,6 @@ int hvk_gemm_gelu_fwd(const void* x, const void* w, const float* bias, void* h, 
  * w [N, K] (= fc2.weight^T), h [M, N] the saved pre-activation. */
 int hvk_gemm_gelu_bwd(const void* gy, const void* w, const void* h, void* gh, int M, int K, int N,
                       void* stream);
-/* Tile kernel selection for the three entry points above: 0 (default) = the 128 x 128 /
- * 128 x 192 two-workgroups-per-CU kernel only, 1 = the ping-pong 256 x 256 / 128 x 384 kernel
- * (one 8-wave workgroup per CU) wherever its tile divides N, 2 / 3 = only its 256 x 256 /
- * 128 x 384 tile.  Both kernels accumulate in the same order, so their results are
- * bit-identical.  Returns the previous mode (option "gemm_pp", initially 0). */
-int hvk_gemm_set_pp(int mode);
 
 /* ---- Weight-gradient GEMM (the backward of every SwinV2 Linear) ----------------------
  * dw[N, K] = g[M, N]^T x[M, K] in f32 and, when db is not NULL, db[N] = sum_m g[m, n]

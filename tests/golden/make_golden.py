@@ -1,7 +1,7 @@
 """Generate the golden fixtures under tests/golden/ by importing the REFERENCE
 (/root/reference, read-only) in the build container.
 
-Run:  python tests/golden/make_golden.py [--only index,modules,models,taxonomy,losses,swinb,prod,steps]
+Run:  python tests/golden/make_golden.py [--only index,modules,models,taxonomy,losses,swinb,prod,steps,prodb,step256]
       (needs /root/reference; CPU only)
 
 The reference's third-party imports that are absent offline are replaced by
@@ -112,6 +112,10 @@ def main():
         swinb_and_prod(ref, init_params_from_rng, "prod")
     if "steps" in only:
         train_steps(ref, ref_h, init_params_from_rng)
+    if "prodb" in only:
+        bench_batch_modules(ref, init_params_from_rng)
+    if "step256" in only:
+        train_step_b256(ref, init_params_from_rng)
     if "index" not in only:
         return main_rest(ref, ref_h, only)
     # ---------------------------------------------------------------- indices
@@ -476,6 +480,111 @@ def train_steps(ref, ref_h, init_params_from_rng):
             out[f"{name}.e16.{k}"] = np.array(float((g16 - g32).norm() / g32.norm().clamp_min(1e-30)))
         del net, grads
     np.savez_compressed(os.path.join(HERE, "step_golden.npz"), **out)
+
+
+BENCH_BLOCKS = {
+    # SwinV2-T stages 1-3 at the batch sizes where the product takes its bench routing
+    # (hvamd/ops.py _tile_ok: the tiled GEMMs from M >= 32768 tokens at stages 1-2, M >= 8192 at
+    # stage 3, the stage-1 norm in the 128 x 192 tile's epilogue, the qkv normalisation epilogue)
+    "t_s1_b48": dict(dim=192, res=28, heads=6, window=7, shift=3, batch=48, seed=130),
+    "t_s2_b168": dict(dim=384, res=14, heads=12, window=7, shift=3, batch=168, seed=140),
+    "t_s3_b192": dict(dim=768, res=7, heads=24, window=7, shift=0, batch=192, seed=150),
+    # a ragged token count (M = 176 x 49, not a multiple of the weight-gradient kernel's 32-token
+    # stage): the dW launches split into an aligned part and a zero-padded tail
+    "t_s3_b176": dict(dim=768, res=7, heads=24, window=7, shift=0, batch=176, seed=155),
+}
+BENCH_MERGES = {
+    # the three SwinV2-T PatchMergings at the same sizes (gather folded into the reduction GEMM;
+    # the stage-0 -> 1 one with its norm in the tile epilogue)
+    "m01_b48": dict(dim=96, res=56, batch=48, seed=160),
+    "m12_b168": dict(dim=192, res=28, batch=168, seed=170),
+    "m23_b192": dict(dim=384, res=14, batch=192, seed=180),
+    "m23_b176": dict(dim=384, res=14, batch=176, seed=185),  # ragged: gather + tile GEMM, split dW
+}
+
+
+def bench_batch_modules(ref, init_params_from_rng):
+    """prodb_golden.npz: BENCH_BLOCKS / BENCH_MERGES in f32 (sampled output, input gradient and
+    every parameter gradient) plus the reference's own CPU bf16-autocast error per tensor
+    (relative L2 over the full tensor), from which the tests derive their bounds."""
+    out = {}
+    mods = [(n, c, "block") for n, c in BENCH_BLOCKS.items()] + [(n, c, "merge") for n, c in BENCH_MERGES.items()]
+    for name, c, kind in mods:
+        if kind == "block":
+            m = ref.SwinTransformerBlock(dim=c["dim"], input_resolution=(c["res"], c["res"]), num_heads=c["heads"],
+                                         window_size=c["window"], shift_size=c["shift"])
+        else:
+            m = ref.PatchMerging((c["res"], c["res"]), dim=c["dim"])
+        shapes = {k: v.shape for k, v in m.state_dict().items()
+                  if v.dtype.is_floating_point and not k.endswith("logit_clamp_max")
+                  and "relative_coords_table" not in k and "attn_mask" not in k}
+        m.load_state_dict(init_params_from_rng(shapes, c["seed"]), strict=False)
+        L = c["res"] * c["res"]
+        xin = torch.from_numpy(seeded(c["seed"] + 1, (c["batch"], L, c["dim"])))
+        res = {}
+        for prec in ("f32", "bf16"):
+            m.zero_grad(set_to_none=True)
+            x = xin.clone().requires_grad_(True)
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=prec == "bf16"):
+                y = m(x)
+            gy = torch.from_numpy(seeded(c["seed"] + 2, tuple(y.shape)))
+            y.float().backward(gy)
+            res[prec] = {"y": y.detach().float(), "gx": x.grad.float()}
+            res[prec].update({"grad." + k: v.grad.detach().float().clone() for k, v in m.named_parameters()})
+        pre = name + "."
+        for k, a in res["f32"].items():
+            out[pre + k] = sampled(pre + k, a.numpy())
+            out[pre + "e16." + k] = np.array(float((res["bf16"][k] - a).norm() / a.norm().clamp_min(1e-30)))
+        print(name, {k: round(float(out[pre + "e16." + k]), 4) for k in res["f32"]}, flush=True)
+    np.savez_compressed(os.path.join(HERE, "prodb_golden.npz"), **out)
+
+
+STEP256 = dict(img_size=224, embed_dim=96, depths=[2, 2, 6, 2], num_heads=[3, 6, 12, 24], window_size=7,
+               num_classes=10000, drop_path_rate=0.0)
+STEP256_BATCH, STEP256_CHUNK = 256, 32
+
+
+def train_step_b256(ref, init_params_from_rng):
+    """step256_golden.npz: the bench's own step (BASELINE configs[2]: SwinV2-T 224 + HXE over the
+    10 000-leaf tree, batch 256) on the reference network, f32 and CPU bf16 autocast: loss and
+    every parameter gradient (sampled) plus the reference's own bf16 error per tensor.  The batch
+    runs as 8 chunks of 32 with each chunk's loss scaled by 32/256 and the gradients accumulated
+    (the same sum as one batch of 256, in 8 pieces, so the reference's CPU activations fit this
+    container's memory).  HXE is the oracle's (hierarchy.py:183-185 raises), as in train_steps."""
+    sys.path.insert(0, REPO)
+    from oracle import hierarchy_ref
+    from hvamd.hierarchy import Taxonomy
+    tax = Taxonomy.synthetic()
+    lam = hierarchy_ref.hxe_level_weights("exponential", 0.1)
+    net = ref.SwinTransformerV2(**STEP256).train()
+    shapes = {k: v.shape for k, v in net.state_dict().items()
+              if k.endswith(("weight", "bias", "logit_scale")) and "relative" not in k}
+    missing, unexpected = net.load_state_dict(init_params_from_rng(shapes, 7), strict=False)
+    assert not unexpected, unexpected
+    B, CH = STEP256_BATCH, STEP256_CHUNK
+    x = seeded(42, (B, 3, 224, 224))
+    leaves = np.random.default_rng(43).integers(0, tax.num_leaves, B)
+    paths = tax.leaf_paths[leaves]
+    out = {"t256.leaves": leaves, "t256.x_checksum": np.array([float(x.astype(np.float64).sum()),
+                                                               float(np.abs(x).astype(np.float64).sum())])}
+    grads = {}
+    for prec in ("f32", "bf16"):
+        net.zero_grad(set_to_none=True)
+        total = 0.0
+        for c0 in range(0, B, CH):
+            with torch.autocast("cpu", dtype=torch.bfloat16, enabled=prec == "bf16"):
+                z = net(torch.from_numpy(x[c0:c0 + CH]))
+            loss = hierarchy_ref.hxe_loss_torch(z.float(), paths[c0:c0 + CH], tax.perm, tax.node_start,
+                                                tax.node_end, tax.tier_base, lam) * (CH / B)
+            loss.backward()
+            total += float(loss)
+            print("t256", prec, c0, float(loss), flush=True)
+        out[f"t256.loss_{prec}"] = np.array(total)
+        grads[prec] = {k: v.grad.detach().float().clone() for k, v in net.named_parameters() if v.grad is not None}
+    for k, g32 in grads["f32"].items():
+        out[f"t256.g.{k}"] = sampled(f"t256.g.{k}", g32.numpy(), STEP_SAMPLES)
+        out[f"t256.e16.{k}"] = np.array(float((grads["bf16"][k] - g32).norm() / g32.norm().clamp_min(1e-30)))
+    np.savez_compressed(os.path.join(HERE, "step256_golden.npz"), **out)
 
 
 class _FakeDir(str):

@@ -242,3 +242,48 @@ def test_grad_accum_validation():
     assert [tuple(p[1].tolist()) for p in parts] == [(0, 1), (2, 3), (4, 5)]
     with pytest.raises(ValueError, match="equal microbatches"):
         _split_batch((x, y), 4)
+
+
+def _train_comm(rank, world, port, out):
+    """Trainer.comm_timing on two gloo ranks: every step records the backward's start / end, each
+    bucket's all-reduce enqueue and the point after buckets.synchronize(); comm_report turns them
+    into the bench line's `comm` fields."""
+    from hvamd.algorithmic import GradientClipping
+    from hvamd.hierarchy import Taxonomy
+    from hvamd.optim import DecoupledSGDW, set_weight_decay
+    from hvamd.trainer import Trainer, comm_report
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    tax = Taxonomy.synthetic(TAX_SIZES)
+    model = _OracleSwin(tax)
+    opt = DecoupledSGDW(set_weight_decay(model), lr=0.05, momentum=0.9, weight_decay=5e-4)
+    trainer = Trainer(model, opt, [GradientClipping("norm", 1.0)], bucket_mb=0.05)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 3, 56, 56, generator=g)
+    y = torch.from_numpy(tax.leaf_paths[[1, 5, 9, 11]])
+    shard = slice(rank * 2, rank * 2 + 2)
+    trainer.train_step((x[shard], y[shard]))
+    trainer.comm_timing = []
+    for _ in range(2):
+        trainer.train_step((x[shard], y[shard]))
+    rep = comm_report(trainer.comm_timing)
+    out[rank] = (rep, len(trainer.buckets.buckets), trainer.buckets.trace)
+    dist.destroy_process_group()
+
+
+def test_comm_timing_world2():
+    """The bench's `comm` block on a world-2 gloo run: exposed exchange time >= 0 and shorter than
+    a step, one enqueue offset per bucket, all >= 0 (every all-reduce is enqueued before the
+    backward ends and at most a backward's length before it)."""
+    out = mp.Manager().dict()
+    mp.spawn(_train_comm, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        rep, nb, trace = out[r]
+        assert trace is None
+        assert rep["steps"] == 2 and nb > 2
+        assert 0 <= rep["exposed_ms"] <= rep["exposed_ms_max"] < 60_000
+        assert rep["backward_ms"] > 0
+        offs = rep["bucket_enqueue_before_bwd_end_ms"]
+        assert len(offs) == nb and all(o is not None and o >= 0 for o in offs), offs
+        assert max(offs) <= rep["backward_ms"] + 1.0

@@ -179,63 +179,6 @@ def test_gemm_tile_widths_bit_identical(M, K, N):
     assert torch.equal(out[0].view(torch.int16), out[1].view(torch.int16))
 
 
-@pytest.mark.parametrize("M,K,N,epi", [(50176, 384, 1152, 0), (50176, 1536, 384, 0), (50171, 384, 384, 0),
-                                       (12544, 768, 2304, 0), (12544, 3072, 768, 0), (12544, 2304, 768, 0),
-                                       (50176, 384, 1536, 1), (12544, 768, 3072, 1), (12540, 768, 3072, 1)])
-@pytest.mark.parametrize("xr", [1, 2])
-def test_gemm_xr_bit_identical_to_tile_kernel(M, K, N, epi, xr):
-    """The persistent row-range kernel (gemm_xr.hip, option gemm_xr) accumulates every output in
-    the tile kernel's k order (64-deep steps, two 32-deep MFMAs each) and adds the bias the same
-    way: outputs bit-identical to gemm_nt_kernel's, on a ragged M too (rows past M dropped), for
-    the plain and the fc1 + GELU epilogue; and both within 1e-2 of an fp32 matmul."""
-    from hvamd import _lib
-    lib = _lib.load()
-    g = torch.Generator(device="cuda").manual_seed(M + 3 * K + N + epi)
-    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
-    b = torch.randn(N, device="cuda", generator=g)
-    out = {}
-    for mode in (0, 1):
-        y = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        y2 = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        with _lib.option("gemm_xr", xr if mode else 0):
-            if epi:
-                _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2),
-                          M, K, N, _lib.stream())
-            else:
-                _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), M, K, N, _lib.stream())
-            torch.cuda.synchronize()
-        out[mode] = (y, y2)
-    for i in range(2 if epi else 1):
-        a0, a1 = out[0][i], out[1][i]
-        assert torch.isnan(a1[M:].float()).all()  # nothing written past M
-        assert torch.equal(a0[:M].view(torch.int16), a1[:M].view(torch.int16)), i
-    ref = x.float() @ w.float().t() + b
-    rel = ((out[1][0][:M].float() - ref).norm() / ref.norm()).item()
-    assert rel < 1e-2, rel
-
-
-@pytest.mark.parametrize("M,K,N", [(50176, 384, 1536), (12544, 768, 3072), (50170, 384, 1536)])
-@pytest.mark.parametrize("xr", [1, 2])
-def test_gemm_xr_gelu_bwd_bit_identical_to_tile_kernel(M, K, N, xr):
-    """fc2's input gradient through GELU' (hvk_gemm_gelu_bwd) on the persistent row-range
-    kernel: bit-identical to the tile kernel (same k order, same GELU' of the same h)."""
-    from hvamd import _lib
-    g = torch.Generator(device="cuda").manual_seed(M + K + 5 * N)
-    gy = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
-    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
-    out = {}
-    for mode in (0, 1):
-        gh = torch.full((M + 8, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        with _lib.option("gemm_xr", xr if mode else 0):
-            _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(gy), _lib.ptr(w), _lib.ptr(h), _lib.ptr(gh), M, K, N, _lib.stream())
-            torch.cuda.synchronize()
-        out[mode] = gh
-    assert torch.isnan(out[1][M:].float()).all()
-    assert torch.equal(out[0][:M].view(torch.int16), out[1][:M].view(torch.int16))
-
-
 @pytest.mark.parametrize("N", [384, 256, 192])
 def test_gemm_tile_sparse_pattern_pins_layout(N):
     """One nonzero token row and one nonzero weight row: the output must be exactly one
@@ -426,53 +369,6 @@ def test_attn_biases_match_torch(C):
     assert torch.equal(pb.grad, g)
     assert torch.allclose(w.grad, torch.outer(g, vb.detach()), rtol=1e-6, atol=1e-6)
     assert qb.grad is None
-
-
-@pytest.mark.parametrize("M,K,N", [(50176, 384, 1152), (12544, 768, 768), (777, 1536, 2304),
-                                   (300, 192, 384), (1000, 1152, 384), (3000, 64, 256)])
-@pytest.mark.parametrize("epi", ["plain", "bias", "gelu_fwd", "gelu_bwd"])
-def test_gemm_pingpong_bit_identical_to_two_wg_kernel(M, K, N, epi):
-    """The ping-pong kernel (256 x 256 / 128 x 384 tiles, hvk_gemm_set_pp) accumulates in the
-    same k order as the 128-row tile kernel, so every epilogue form must agree bit for bit;
-    ragged M and single-k-step K included."""
-    from hvamd import _lib
-    lib = _lib.load()
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + K + N)
-    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
-    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
-    b = torch.randn(N, device="cuda", generator=g)
-    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
-    outs = []
-    prev = lib.hvk_gemm_set_pp(0)
-    try:
-        for mode in (0, 1):  # two-workgroup tiles, then ping-pong wherever it divides N
-            lib.hvk_gemm_set_pp(mode)
-            y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-            y2 = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-            if epi in ("plain", "bias"):
-                _lib.call("hvk_gemm_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b) if epi == "bias" else None,
-                          _lib.ptr(y), M, K, N, _lib.stream())
-            elif epi == "gelu_fwd":
-                _lib.call("hvk_gemm_gelu_fwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(b), _lib.ptr(y), _lib.ptr(y2),
-                          M, K, N, _lib.stream())
-            else:
-                _lib.call("hvk_gemm_gelu_bwd", _lib.ptr(x), _lib.ptr(w), _lib.ptr(h), _lib.ptr(y), M, K, N,
-                          _lib.stream())
-            torch.cuda.synchronize()
-            outs.append((y, y2))
-    finally:
-        lib.hvk_gemm_set_pp(prev)
-    (y0, y20), (y1, y21) = outs
-    assert not torch.isnan(y1.float()).any()
-    assert torch.equal(y0.view(torch.int16), y1.view(torch.int16))
-    if epi == "gelu_fwd":
-        assert torch.equal(y20.view(torch.int16), y21.view(torch.int16))
-    ref = x.float() @ w.float().t() + (b if epi in ("bias", "gelu_fwd") else 0)
-    if epi == "gelu_bwd":
-        hf = h.float().requires_grad_(True)
-        torch.nn.functional.gelu(hf).backward(ref)
-        ref = hf.grad
-    assert ((y1.float() - ref).norm() / ref.norm()).item() < 1e-2
 
 
 @pytest.mark.parametrize("M", [802816, 1000, 37])

@@ -6,8 +6,7 @@ reference network in f32 there.  Bounds are derived from the reference itself: t
 1e-2 relative (north star), every parameter gradient within max(2e-2, 1.5 x the reference's OWN
 CPU bf16-autocast error on that tensor) relative L2 (stored per tensor in the fixture, measured
 on the full tensors; for the logit-scale and CPB-MLP gradients, sums of dS cos / dS that cancel
-through the bf16 softmax, max(5e-2, 2 x) as in test_gpu_model.py's mini-model bound: their
-run-to-run spread under the backward's atomic accumulation order alone is ~2 %), all
+through the bf16 softmax, max(5e-2, 1.5 x) as in test_gpu_model.py's mini-model bound), all
 gradients together within max(2e-2, the reference's own bf16-autocast error on the same sampled
 elements, estimated from its per-tensor errors: t_hxe 0.028, b224_mt 0.020, b384_hxe 0.035).  HXE is not implemented by the
 reference (hierarchy.py:183-185): the fixture's loss on the reference's logits is the oracle's
@@ -73,10 +72,11 @@ def test_train_step_vs_reference(golden, name):
         r = _rel(a, b)
         cancel = "logit_scale" in k or "cpb_mlp" in k
         base = 5e-2 if cancel else BASE
-        # the cancelling sums (dS . cos, dS) take 2x the reference's own bf16 error: with the
-        # W-MSA backward's atomic accumulation order the same build measured 0.0707 and 0.0724
-        # on layers.1.blocks.1.attn.logit_scale (reference's own 0.0472) in two runs
-        lim = max(base, (2.0 if cancel else 1.5) * float(g[f"{name}.e16.{k}"]))
+        # 1.5x the reference's own bf16 error on every tensor, the cancelling sums (dS . cos, dS)
+        # included: the W-MSA backward's parameter-gradient reductions are deterministic (round 6;
+        # with round 5's atomics the same build measured 0.0707 and 0.0724 on
+        # layers.1.blocks.1.attn.logit_scale against the reference's own 0.0472)
+        lim = max(base, 1.5 * float(g[f"{name}.e16.{k}"]))
         worst.append((r / lim, r, lim, k))
         mine.append(a)
         theirs.append(b)
@@ -92,5 +92,13 @@ def test_train_step_vs_reference(golden, name):
     print(f"{name}: loss {loss.item():.6f} vs {ref:.6f} (ref bf16 {ref16:.6f}); all grads {allrel:.4f} "
           f"(reference's own bf16 {ref_all16:.4f}); "
           f"closest to bound (r/lim, r, lim): {[(round(u, 2), round(v, 4), round(w, 4), k) for u, v, w, k in worst[:6]]}")
+    import json
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, f"steps_{name}.json"), "w") as f:
+        json.dump({"loss": loss.item(), "loss_ref_f32": ref, "loss_ref_bf16": ref16, "all_grads_rel": allrel,
+                   "all_grads_ref_bf16": ref_all16,
+                   "worst": [(round(u, 3), round(v, 5), round(w, 5), k) for u, v, w, k in worst[:10]]}, f, indent=1)
     assert not bad, bad
     assert allrel < max(BASE, ref_all16), (allrel, ref_all16)

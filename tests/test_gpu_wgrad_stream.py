@@ -76,3 +76,77 @@ def test_weight_grad_chunk_target(chunks, M, N, K):
     assert ((dw.double() - ref).norm() / ref.norm()).item() < 1e-6
     dbr = gy.double().sum(0)
     assert ((db.double() - dbr).norm() / dbr.norm()).item() < 1e-6
+
+
+def _linear_grads(w, b, x, twice, on):
+    from hvamd import ops, options
+    w.grad = b.grad = None
+    ops.reset_leaf_uses()
+    with options.override(wgrad_stream=on), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.linear(x, w, b)
+        if twice:  # the same parameters in one graph twice: autograd sums their two gradients
+            y = ops.linear(y, w, b)
+        with ops.wgrad_stream_scope():
+            y.float().square().mean().backward()
+    return w.grad.detach().clone(), b.grad.detach().clone()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("twice", [False, True])
+def test_side_stream_refuses_unsafe_leaves(dtype, twice):
+    """a Linear applied twice (tied weights) and bf16 parameters (autograd casts
+    the f32 gradient on the current stream) must not put their gradients on the side stream --
+    the gradients equal the side-stream-off run, and the fork count does not move for them."""
+    from hvamd import ops
+    torch.manual_seed(3)
+    w = torch.nn.Parameter((torch.randn(192, 192, device="cuda") / 14).to(dtype))
+    b = torch.nn.Parameter(torch.randn(192, device="cuda").to(dtype))
+    x = torch.randn(4096, 192, device="cuda")
+    ref = _linear_grads(w, b, x, twice, False)
+    f0 = ops.wgrad_fork_count()
+    got = _linear_grads(w, b, x, twice, True)
+    forked = ops.wgrad_fork_count() - f0
+    torch.cuda.synchronize()
+    assert forked == (1 if dtype == torch.float32 and not twice else 0), forked
+    for a, r in zip(got, ref):
+        assert torch.equal(a.float(), r.float())
+
+
+def test_bucket_hook_takes_no_wait_path_for_side_gradients():
+    """a gradient written on the side stream is recognised by storage (autograd
+    stores a detached alias), so GradientBuckets' hook copies it without making the side stream
+    wait on the current one; a parameter-gradient the current stream wrote is not."""
+    from hvamd import ops
+    blk = _block(96, 3)
+    x = torch.randn(2, 28 * 28, 96, device="cuda")
+    seen = {}
+
+    def hook(name):
+        def h(p):
+            seen[name] = (ops.wgrad_side_pending() is not None, ops.wgrad_produced_on_side(p.grad))
+        return h
+    hs = [blk.mlp.fc1.weight.register_post_accumulate_grad_hook(hook("fc1")),
+          blk.norm1.weight.register_post_accumulate_grad_hook(hook("norm1"))]
+    ops.reset_leaf_uses()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = blk(x)
+    with ops.wgrad_stream_scope():
+        y.float().square().mean().backward()
+    torch.cuda.synchronize()
+    for h in hs:
+        h.remove()
+    assert seen["fc1"] == (True, True), seen
+    assert seen["norm1"][1] is False, seen  # the LayerNorm column sums ran on the current stream
+
+
+def test_ln_column_sums_on_side_stream_equal():
+    """options.wgrad_stream_ln (hvk_ln_residual_bwd_split: the LayerNorm
+    backward's column sums on the side stream) gives the same gradients as the single-stream
+    kernel: same kernels, same partial sums (the CPB chain's atomics aside, as in _compare)."""
+    from hvamd import options
+    blk = _block(192, 6)
+    x = torch.randn(8, 28 * 28, 192, device="cuda")
+    g0 = _grads(blk, x, True)
+    with options.override(wgrad_stream_ln=True):
+        g1 = _grads(blk, x, True)
+    _compare(g0, g1)

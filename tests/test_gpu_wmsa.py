@@ -227,9 +227,9 @@ def test_wmsa_backward_slices_and_nontemporal_reads_agree(B, H, W, nh, win, shif
     """The w <= 8 backward's other launch paths give the default path's bits: the batch-slice
     loop (taken when qkv exceeds the 2 GiB buffer-descriptor range; here forced with option
     wmsa_bwd_slice_bytes at 1, 2 and 3 images per slice) and the nontemporal qkv reads
-    (wmsa_bwd_nt = 1).  dqkv is written without atomics, so it must match bit for bit; the
-    CPB-table / scale / q_bias gradients sum per-workgroup atomics in launch order, so they are
-    compared at 1e-5."""
+    (wmsa_bwd_nt = 1).  dqkv must match bit for bit; the CPB-table / scale / q_bias gradients are
+    summed over a different window-to-chunk split when the batch is sliced, so they are compared at
+    1e-5 (each run is deterministic: test_wmsa_backward_param_grads_deterministic)."""
     import hvamd._lib as lib
     import hvamd.ops as ops
     qkv, tab, scale = _inputs(B, H, W, nh, win, 9)
@@ -346,3 +346,27 @@ def test_wmsa_forward_head_groups_bit_identical(B, H, W, nh, win, shift):
     assert torch.isfinite(outs[0].float()).all()
     for hg, o in outs.items():
         assert torch.equal(o.view(torch.int16), outs[0].view(torch.int16)), hg
+
+
+@pytest.mark.parametrize("B,H,W,nh,win,shift", [(4, 28, 28, 3, 7, 3), (3, 14, 14, 12, 7, 3), (2, 16, 16, 2, 8, 4),
+                                                (1, 48, 48, 2, 24, 12), (2, 24, 24, 4, 12, 0)])
+def test_wmsa_backward_param_grads_deterministic(B, H, W, nh, win, shift):
+    """the CPB-table, logit-scale and q_bias gradients come from per-(chunk,
+    head) workspace slots summed in chunk order (no float atomics), so two runs give the same bits,
+    like dqkv."""
+    import hvamd.ops as ops
+    qkv, tab, scale = _inputs(B, H, W, nh, win, 12)
+    gout = torch.from_numpy(np.random.default_rng(13).standard_normal((B, H * W, 32 * nh)).astype(np.float32))
+
+    def run():
+        q = qkv.cuda().bfloat16().requires_grad_(True)
+        t, s = tab.cuda().requires_grad_(True), scale.cuda().requires_grad_(True)
+        qb = torch.zeros(32 * nh, device="cuda", requires_grad=True)
+        ops.window_attention_core(q, t, s, H, W, nh, win, shift, q_bias=qb).backward(gout.cuda().bfloat16())
+        torch.cuda.synchronize()
+        return [x.grad.float().cpu() for x in (q, t, s, qb)]
+
+    a, b = run(), run()
+    for name, x, y in zip(("dqkv", "dbias", "dscale", "dq_bias"), a, b):
+        assert torch.isfinite(x).all(), name
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32)), name

@@ -33,8 +33,9 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     assert lib.hvk_abi_version() == _lib.ABI_VERSION
     # [accumulators][dscale nH][dq_bias 32 nH] floats
-    assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == (3 * 16 * 256 + 3 * 33) * 4
-    assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == (4 * 47 * 47 + 4 * 33) * 4
+    # [heads][slots: 512 / heads][R*R CPB bins, d scale, 32 d q_bias] f32 (deterministic reduction)
+    assert lib.hvk_wmsa_bwd_workspace_bytes(3, 7) == 3 * (512 // 3) * (13 * 13 + 33) * 4
+    assert lib.hvk_wmsa_bwd_workspace_bytes(4, 24) == 4 * 64 * (47 * 47 + 33) * 4
     # weight-gradient plan: one tile, 256 token chunks of [dW | db] partials
     assert lib.hvk_weight_grad_supported(802816, 288, 96) == 1
     assert lib.hvk_weight_grad_workspace(802816, 288, 96) == 256 * (288 * 96 + 288) * 4
@@ -107,7 +108,7 @@ def test_library_options_table():
     values are refused."""
     from hvamd import _lib
     defaults = {"wmsa_fwd_form": 0, "wmsa_bwd_nt": 0, "wmsa_bwd_slice_bytes": 1 << 31,
-                "gemm_pp": 0, "tile_wide": -1, "dw_tile": 5}
+                "tile_wide": -1, "dw_tile": 5, "wmsa_fwd_hg": 0, "dw_chunks": 256}
     for name, v in defaults.items():
         assert _lib.get_option(name) == v, name
     with _lib.option("wmsa_fwd_form", 1):
@@ -116,7 +117,9 @@ def test_library_options_table():
     for name, bad in [("wmsa_fwd_form", 2), ("dw_tile", 3), ("no_such_option", 0)]:
         with pytest.raises(RuntimeError):
             _lib.set_option(name, bad)
-    assert _lib.load().hvk_gemm_set_pp(0) == 0
+    for gone in ("gemm_pp", "gemm_xr", "gemm_wide"):  # the measured-slower GEMM forms were removed (round 6)
+        with pytest.raises(RuntimeError):
+            _lib.get_option(gone)
     src = os.path.join(ROOT, "hierarchical-vision_amd", "csrc")
     for f in os.listdir(src):
         if f.endswith((".hip", ".h")):

@@ -42,29 +42,19 @@ def main():
     print(f"buckets: {len(trainer.buckets.buckets)} "
           f"({', '.join(f'{b[0].numel() * 4 / 2**20:.1f}' for b in trainer.buckets.buckets)} MB)", flush=True)
     batch = bench.synthetic_batch(A, tax, 0, dev)
-    # GPU-timeline position of each bucket's all-reduce enqueue (a timing event recorded on the
-    # producing stream right before dist.all_reduce: RCCL's stream waits on that point, so the
-    # all-reduce can run from there on) against the step's start and the end of the backward
-    # (the last bucket's enqueue follows the last gradient)
     sizes = [b[0].numel() * 4 / 2**20 for b in trainer.buckets.buckets]
+    # GPU-timeline position of each bucket's all-reduce enqueue (a timing mark on the producing
+    # stream right before dist.all_reduce: RCCL's stream waits on that point) against the end of
+    # the backward, and the exposed exchange after it (Trainer.comm_timing / trainer.comm_report)
+    from hvamd.trainer import comm_report
+    trainer.train_step(batch)  # warm-up
+    trainer.comm_timing = []
     for i in range(a.steps):
-        torch.cuda.synchronize()
-        trainer.buckets.trace = []
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev0.record()
         trainer.train_step(batch)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev1.record()
-        torch.cuda.synchronize()
-        tr, trainer.buckets.trace = trainer.buckets.trace, None
-        if i == 0:
-            continue  # warm-up
-        tend = max(ev0.elapsed_time(e) for _, e in tr)
-        print(f"step {i}: step {ev0.elapsed_time(ev1):.2f} ms, backward's last gradient at {tend:.2f} ms")
-        for bi, e in tr:
-            t = ev0.elapsed_time(e)
-            print(f"   bucket {bi} ({sizes[bi]:6.1f} MB) all-reduce enqueued at {t:7.2f} ms = "
-                  f"{tend - t:6.2f} ms before the backward ends")
+    rep = comm_report(trainer.comm_timing)
+    print(rep)
+    for bi, off in enumerate(rep["bucket_enqueue_before_bwd_end_ms"]):
+        print(f"   bucket {bi} ({sizes[bi]:6.1f} MB) all-reduce enqueued {off} ms before the backward ends")
     print("ok", flush=True)
     dist.destroy_process_group()
 
