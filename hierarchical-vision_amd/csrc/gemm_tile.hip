@@ -606,7 +606,10 @@ int launch_tile(const hvk_bf16* X, const hvk_bf16* W, const float* bias, hvk_bf1
   // forces 128 / 192 columns where both divide N
   const int force = (int)hvk_opt(HVK_OPT_TILE_WIDE);
   if constexpr (EPI == 4) {  // the qkv form: the 128-row tile kernel only
-    if (N % TileCfg<6>::BN == 0 && (force >= 0 ? force == 1 : (N > 384 || K >= 1152)))
+    // 192 columns where 192 | N and either 128 does not divide N (N = 192, 576, ...) or the rule
+    // / option asks for them
+    if (N % TileCfg<6>::BN == 0 &&
+        (N % TileCfg<4>::BN != 0 || (force >= 0 ? force == 1 : (N > 384 || K >= 1152))))
       return launch_tile_<EPI, true, 6>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
     return launch_tile_<EPI, true, 4>(X, W, bias, Y, Y2, M, N, K, st, rn, qscale);
   } else {

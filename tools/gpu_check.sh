@@ -17,7 +17,7 @@ import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_ste
 if [ -z "$NO_DP2" ]; then
 timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 5 --warmup 2 --cpu-baseline 0 > $O/dp2.json 2> $O/dp2.err || { tail -30 $O/dp2.err; exit 1; }
 python3 -c "
-import json; d=json.load(open('$O/dp2.json')); print(d['value'], d['comm'])"
+import json; d=json.loads(open('$O/dp2.json').read().strip().splitlines()[-1]); print(d['value'], d['comm'])"
 fi
 if [ -z "$NO_PROF" ]; then
   PROF_OUT=${CK_OUT:-check}/prof bash tools/gpu_prof.sh > /dev/null || exit 1

@@ -9,7 +9,7 @@ mkdir -p $O
 cd $R
 timeout -k 10 300 python tools/bench_wmsa.py --b384 --iters 5 > $O/base.txt 2>&1 || { cat $O/base.txt; exit 1; }
 cat $O/base.txt
-for v in ${PROBES:-lprobe1 lprobe4 lprobe5}; do
+for v in ${PROBES:-}; do  # probe builds (abl/lprobe*.so) when PROBES names them
   echo "== $v" | tee $O/$v.txt
   HVK_LIB_PATH=$R/abl/$v.so timeout -k 10 200 python tools/bench_wmsa.py --b384 --iters 5 --stage 2 --only bwd >> $O/$v.txt 2>&1 || { cat $O/$v.txt; exit 1; }
   cat $O/$v.txt
