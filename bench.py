@@ -401,6 +401,13 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     fallbacks = ops.library_fallbacks(reset=True)  # warm-up + timed steps
+    # caching-allocator health over the warm-up + timed steps: a step that needs more than the
+    # card holds makes the allocator free its cache and retry (a device-wide sync per retry)
+    ms = torch.cuda.memory_stats(device)
+    memory = {"peak_reserved_gib": round(torch.cuda.max_memory_reserved(device) / 2**30, 1),
+              "peak_allocated_gib": round(torch.cuda.max_memory_allocated(device) / 2**30, 1),
+              "alloc_retries": int(ms.get("num_alloc_retries", 0)), "device_allocs": int(ms.get("num_device_alloc", 0)),
+              "device_frees": int(ms.get("num_device_free", 0))}
     comm = None
     if world > 1 and not args.graph and args.comm_steps > 0:
         # the exchange's exposed time and each bucket's overlap window, on extra steps after the
@@ -476,6 +483,7 @@ def main():
         "final_loss": round(loss_val, 4),
         # launches that left libhvk for a torch / hipBLASLt op over the warm-up + timed steps
         "library_fallbacks": {"steps": args.warmup + args.steps, "sites": fallbacks},
+        "memory": memory,
         # every routing switch the run used: host (hvamd.options) and library (hvk_set_option)
         "options": {"host": options.as_dict(), "lib": _lib.options()},
         # whole-step MFMA utilisation: 3 x 2 x MACs per image (forward + both backward GEMMs)

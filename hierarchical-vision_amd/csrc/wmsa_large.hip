@@ -471,6 +471,12 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
 // phase 2's q / dO rows, phase 2 the next window's k / v rows) and written to LDS between the
 // phases; every tile's own global inputs are loaded one tile ahead.  Interior windows and
 // unshifted blocks run mask-free copies of both loops.
+#ifndef HVK_LARGE_LATE_ROWS  // 1: the next phase's image rows loaded after the current phase's loop
+#define HVK_LARGE_LATE_ROWS 1   // (frees their 40 VGPRs inside the loops; their latency is exposed)
+#endif
+#ifndef HVK_LARGE_TR_EARLY     // 1: phase 2's transposed dV / dK fragments read before the bins
+#define HVK_LARGE_TR_EARLY 1
+#endif
 #ifndef HVK_LARGE_PROBE  // tools/ timing probes of the backward (results wrong): 1 no CPB bins, 2 no
                          // row-constant reads, 3 phase 1 skipped, 4 phase 2 skipped
 #define HVK_LARGE_PROBE 0
@@ -508,7 +514,7 @@ __device__ __forceinline__ void pair_swap_f32(const hvk_f32x4& t0, const hvk_f32
 // post)) rn over the lane's 8 channels (x: the raw row slice at hvk_pair_col(gq), dxh: the same
 // channels); the 4 lanes of the row reduce the dot product.  acc (optional): column sums.
 __device__ __forceinline__ void normalize_bwd16(const uint4& xraw, float rn, const float dxh[8], float post,
-                                                hvk_bf16* dst, float* acc) {
+                                                 hvk_bf16* dst, float* acc) {
   float x[8], dot = 0.f;
   hvk_unpack8(xraw, x);
 #pragma unroll
@@ -663,7 +669,9 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     }
   };
 
-  float dscale = 0.f;  // sum dS (S' - c) over the run = sc2 sum dS cos
+  // sum dS (S' - c) over the run = sc2 sum dS cos, from phase 2's f32 dS (the same sum from
+  // phase 1's q^ . dq^ goes through bf16 dS and lost 3 % of this cancelling sum at scale 100)
+  float dscale = 0.f;
   float dqb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float* pb = bins + wave * F::RRP;
 
@@ -704,7 +712,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     // the first tile's inputs before phase 2's rows: in-order wait counts then never make a
     // tile wait for the row prefetch (issued next, consumed after the phase)
     QIn cur = load_qt(wave);
-    load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
+    if (!HVK_LARGE_LATE_ROWS) load_rows(b, wh, ww, 0, -1);  // phase 2's q / dO rows, under phase 1
 #if HVK_LARGE_PROBE == 3  // probe: phase 1 skipped (timing only)
     for (int qt = K::NT; qt < K::NT; qt += F::WAVES) {
 #else
@@ -718,12 +726,13 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       float rnq;
       const uint4 qs = l2_normalize_seq(cur.q, rnq, sc2);
       float rowc, delta;  // row constant (rel. to M_h) and delta for dS
-      // S' (masked) and dP of (chunk c, half t)
-      auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d) {
+      // S' (masked) and dP - d0 of (chunk c, half t): d0 (the row's delta, or 0) enters the dP
+      // MFMA as its C operand
+      auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d, float d0) {
         constexpr bool EDGE = decltype(edge_t)::value;
         const float* tp = mtab + (tq + ky * K::R + kx);
         s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), qs, hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
-        d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), cur.dof, hvk_f32x4{0, 0, 0, 0});
+        d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), cur.dof, hvk_f32x4{-d0, -d0, -d0, -d0});
         if (EDGE) {
           const bool rmis = edge_r && ((ky >= lim) != (qy >= lim));
 #pragma unroll
@@ -755,7 +764,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
               hvk_f32x4 s, d;
-              tile(edge_t, c, t, ky[t], kx[t], s, d);
+              tile(edge_t, c, t, ky[t], kx[t], s, d, 0.f);
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
                 const float p = __builtin_amdgcn_exp2f(s[r]);
@@ -779,8 +788,8 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
               const int kp = 32 * c + 16 * t + 4 * gq;
-              if (edge) tile(std::true_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t]);
-              else tile(std::false_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t]);
+              if (edge) tile(std::true_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t], 0.f);
+              else tile(std::false_type{}, c, t, kp / WIN, kp % WIN, s[t], d[t], 0.f);
             }
             hvk_settle(s[0], s[1], d[0], d[1]);
             float mc = -INFINITY;
@@ -818,11 +827,11 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             hvk_f32x4 s, d;
-            tile(edge_t, c, t, ky[t], kx[t], s, d);
+            tile(edge_t, c, t, ky[t], kx[t], s, d, delta);  // d = dP - delta
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               p[4 * t + r] = __builtin_amdgcn_exp2f(s[r] - rowc);  // padding keys: 0
-              ds[4 * t + r] = p[4 * t + r] * (d[r] - delta);
+              ds[4 * t + r] = p[4 * t + r] * d[r];
               if (LSE) lk += ds[4 * t + r];
             }
           }
@@ -848,7 +857,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       }
       if (gq == 0) {
         lse_s[pos] = rowc;
-        dlt_s[pos] = dlt;
+        dlt_s[pos] = -dlt;  // phase 2's dP MFMA takes -delta as its C operand
       }
       // dq^ = scale (sum_k dS k^ - corr sum_k P k^) in this lane's 8 output channels
       hvk_f32x4 e0, e1;
@@ -862,6 +871,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       normalize_bwd16(cur.qx, rnq, dxh, 1.f, a.dqkv + (size_t)cur.row * C3 + h * 32 + pcol, dqb);
       cur = nxt;
     }
+    if (HVK_LARGE_LATE_ROWS) load_rows(b, wh, ww, 0, -1);
     lds_barrier();             // phase-1 reads done; row constants published
     write_rows(sc2);           // q^ scale log2e (exactly the forward's operand), dO
     lds_barrier();
@@ -881,7 +891,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       return t;
     };
     KIn kc = load_kt(wave);
-    if (w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
+    if (!HVK_LARGE_LATE_ROWS && w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);  // the next window's k / v, under phase 2
 #if HVK_LARGE_PROBE == 4  // probe: phase 2 skipped (timing only)
     for (int kt = K::NT; kt < K::NT; kt += F::WAVES) {
 #else
@@ -900,21 +910,34 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
         constexpr bool EDGE = decltype(edge_t)::value;
         for_chunks([&](int c, const int (&qyy)[2], const int (&qxx)[2]) {
           float p[8], ds[8];
+          // TR_EARLY: the dV / dK operands (transposed dO / q^ fragments) read up front: the compiler
+          // may not move LDS reads across the bins' read-add-write below, where each read exposes
+          // its whole latency in front of its MFMA
+          uint4 tv[2], tkf[2];
+          if (HVK_LARGE_TR_EARLY) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+              tv[dt] = tr_frag(img1, c, dt, li, gq);
+              tkf[dt] = tr_frag(img0, c, dt, li, gq);
+            }
+          }
+
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             const int q0 = 32 * c + 16 * t + 4 * gq;  // this lane's queries q0 .. q0 + 3
             const int bq = (qyy[t] + WIN - 1) * K::R + qxx[t] + WIN - 1;
             const float* tp = mtab + (tk - bq);  // entries tp[-r]
             const hvk_f32x4 c4 = {tp[0], tp[-1], tp[-2], tp[-3]};
-            hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), kh, c4);
-            const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), kc.v, hvk_f32x4{0, 0, 0, 0});
 #if HVK_LARGE_PROBE == 2  // probe: row constants not read (wrong values, timing only)
             const float4 l4 = make_float4(rnk, rnk, rnk, rnk), d4 = l4;
 #else
             const float4 l4 = *reinterpret_cast<const float4*>(lse_s + q0);
-            const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);
+            const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + q0);  // -delta
 #endif
-            const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
+            hvk_f32x4 s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), kh, c4);
+            const hvk_f32x4 d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), kc.v,
+                                           hvk_f32x4{d4.x, d4.y, d4.z, d4.w});  // dP - delta
+            const float lr[4] = {l4.x, l4.y, l4.z, l4.w};
             if (EDGE) {
               const bool rmis = edge_r && ((ky >= lim) != (qyy[t] >= lim));
 #pragma unroll
@@ -926,7 +949,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float pr = __builtin_amdgcn_exp2f(s[r] - lr[r]);  // padding query: lse +inf
-              const float dsr = pr * (d[r] - dr[r]);
+              const float dsr = pr * d[r];
               p[4 * t + r] = pr;
               ds[4 * t + r] = dsr;
               dscale = fmaf(dsr, s[r] - c4[r], dscale);
@@ -966,8 +989,8 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
                                        hvk_pack2(ds[4], ds[5]), hvk_pack2(ds[6], ds[7]));
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
-            dv[dt] = hvk_mfma16(tr_frag(img1, c, dt, li, gq), pf, dv[dt]);
-            dk[dt] = hvk_mfma16(tr_frag(img0, c, dt, li, gq), dsf, dk[dt]);
+            dv[dt] = hvk_mfma16(HVK_LARGE_TR_EARLY ? tv[dt] : tr_frag(img1, c, dt, li, gq), pf, dv[dt]);
+            dk[dt] = hvk_mfma16(HVK_LARGE_TR_EARLY ? tkf[dt] : tr_frag(img0, c, dt, li, gq), dsf, dk[dt]);
           }
         });
       };
@@ -982,6 +1005,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       hvk_st16(dst + 2 * C + pcol, vk);
       kc = kn;
     }
+    if (HVK_LARGE_LATE_ROWS && w + 1 < w1) load_rows(cb, cwh, cww, 1, 2);
     lds_barrier();  // phase-2 reads done
     if (w + 1 < w1) {
       write_rows(1.f);  // the next window's k^, v
