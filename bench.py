@@ -64,6 +64,9 @@ def parse():
                     help="run on a stream of this priority (negative = higher than the side stream's)")
     ap.add_argument("--host-opt", action="append", default=[], metavar="NAME=VALUE",
                     help="set a host routing option (hvamd.options) before the run; A/B runs")
+    ap.add_argument("--steps-in-flight", type=int, default=-1,
+                    help="eager steps the host may enqueue ahead of the GPU (Trainer.max_steps_in_flight; "
+                         "0: unbounded; default: the Trainer's)")
     ap.add_argument("--comm-steps", type=int, default=5,
                     help="world > 1: extra eager steps after the timed region that record the "
                          "exchange's exposed time and bucket enqueue points (the `comm` block)")
@@ -363,6 +366,8 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=args.stream_priority))
 
     cfg, tax, model, trainer = build(args, device)
+    if args.steps_in_flight >= 0:
+        trainer.max_steps_in_flight = args.steps_in_flight or None
     img = model.module.patch_embed.img_size[0]
     batch = synthetic_batch(args, tax, rank, device, img)
 

@@ -134,7 +134,7 @@ class GradientBuckets:
             g = p.grad
             v.copy_(g)
             if side is not None:
-                g.record_stream(side)
+                ops.wgrad_hold(g)  # freed after the join (ops.wgrad_hold)
             p.grad = v
         if self.accumulating:  # later microbatches add onto the view in place
             return

@@ -179,6 +179,7 @@ class _WgradStream:
     pending = False
     armed = False
     produced = set()  # storage addresses of gradients written on the side stream (until the join)
+    held = []  # tensors the side stream reads / writes that the current stream allocated (until the join)
     uses = {}  # id(parameter) -> forward uses since the last backward join (note_leaf_uses)
     forks = 0  # launches put on the side stream (wgrad_fork_count)
 
@@ -273,13 +274,33 @@ def wgrad_produced_on_side(t):
     return t is not None and t.untyped_storage().data_ptr() in _WgradStream.produced
 
 
-def _wgrad_joined(tensors):
-    """After launches on the side stream that read / write `tensors` (allocated on the main
-    stream): keep their memory until the side stream is done with it, and make sure the main
-    stream waits for the side stream before the backward returns (an autograd final callback;
-    outside a backward, at once)."""
+def wgrad_hold(*tensors):
+    """Keep `tensors` (allocated on the current stream, used by side-stream launches) alive until
+    the join: dropped right after the current stream has waited for the side stream, their blocks go
+    back to the current stream's pool in stream order.  (record_stream instead lets the allocator
+    reuse a block only once the GPU has passed its side-stream use: with the host steps ahead of the
+    GPU every such block stays unavailable and each step maps fresh HBM -- SwinV2-B 384 went from
+    175 to 470-650 ms per step and 287 GB reserved that way.)"""
+    if OPTIONS.wgrad_hold:
+        _WgradStream.held.extend(t for t in tensors if t is not None)
+        return
     side = _WgradStream.side
     for t in tensors:
+        if t is not None:
+            t.record_stream(side)
+
+
+def _wgrad_joined(tensors, outputs=()):
+    """After launches on the side stream that read / write `tensors` (operands and workspaces,
+    allocated on the main stream) and write `outputs` (the gradients handed back to autograd): keep
+    the operands alive until the join (wgrad_hold), protect the outputs' memory with record_stream
+    (they are small; holding a reference would stop AccumulateGrad from stealing them -- it would
+    clone them on the current stream, racing the side stream), and make sure the main stream waits
+    for the side stream before the backward returns (an autograd final callback; outside a
+    backward, at once)."""
+    wgrad_hold(*tensors)
+    side = _WgradStream.side
+    for t in outputs:
         if t is not None:
             t.record_stream(side)
     _WgradStream.pending = True
@@ -301,6 +322,7 @@ def join_wgrad():
     if _WgradStream.pending:
         torch.cuda.current_stream().wait_stream(_WgradStream.side)
         _WgradStream.pending = False
+    _WgradStream.held.clear()  # after the wait: later current-stream reuse is ordered behind the side stream
     _WgradStream.produced.clear()
 
 
@@ -325,7 +347,7 @@ def _dw_launch(g, x, with_db, gelu_x, xs, keep):
     """(dW, db) from hvk_weight_grad / _gelu_x / _shift on the current stream; a ragged M (a
     microbatch whose tokens are not a multiple of the kernel's 32-token stage) runs the aligned
     part and the tail padded with zero rows (a zero g row adds nothing; GELU(0) = 0), summed.
-    Every tensor the launches touch is appended to `keep` (the side stream's record_stream)."""
+    Every tensor the launches touch is appended to `keep` (held until the join: wgrad_hold)."""
     lib = _lib.load()
     M, N = g.shape
     K = x.shape[1]
@@ -343,7 +365,7 @@ def _dw_launch(g, x, with_db, gelu_x, xs, keep):
             call("hvk_weight_grad_shift", ptr(gg), ptr(xx), ptr(xs), ptr(dw), ptr(db), m, N, K, ptr(ws), nb, stream())
         else:
             call("hvk_weight_grad", ptr(gg), ptr(xx), ptr(dw), ptr(db), m, N, K, ptr(ws), nb, stream())
-        keep.extend((gg, xx, dw, db, ws))
+        keep.extend((gg, xx, ws))
         return dw, db
 
     tail = M % _DW_TOK
@@ -356,6 +378,7 @@ def _dw_launch(g, x, with_db, gelu_x, xs, keep):
     dw, db = one(gt, xt)
     if M > tail:
         dw0, db0 = one(g[:M - tail], x[:M - tail])
+        keep.extend((gt, xt, dw, db))  # the tail's partials: read by the adds below
         dw = dw0.add_(dw)
         db = db0.add_(db) if with_db else None
     return dw, db
@@ -375,7 +398,7 @@ def weight_grad(g, x, with_db=False, gelu_x=False, xshift=None, leaves=()):
     keep = [xs]
     with torch.cuda.stream(side):
         dw, db = _dw_launch(g, x, with_db, gelu_x, xs, keep)
-    _wgrad_joined(keep)
+    _wgrad_joined(keep, (dw, db))
     _wgrad_outputs(dw, db)
     return dw, db
 
@@ -1015,8 +1038,8 @@ class BlockTables(torch.autograd.Function):
                  ptr(dtable), ptr(dscale), ptr(dw1), ptr(db1), ptr(dw2), ptr(dlogit), ptr(ws), nbytes,
                  stream())
         if fork:
-            _wgrad_joined((g_eff, v, pw, coords, w1, b1, w2, logit, table, dtable, dscale, dpb, dv, dpw, dw1, db1,
-                           dw2, dlogit))
+            _wgrad_joined((g_eff, v, pw, coords, w1, b1, w2, logit, table, dtable, dscale),
+                          (dpb, dv, dpw, dw1, db1, dw2, dlogit))
             _wgrad_outputs(dv, dpb, dpw, dw1, db1, dw2)
         return (dv, dpb, dpw, None, dw1, db1, dw2, dlogit.reshape(ctx.logit_shape), None, None)
 
@@ -1095,7 +1118,7 @@ def _ln_residual_bwd(a, abias, gamma, sample_scale, mean, rstd, rps, has_x0, gx,
     call("hvk_ln_residual_bwd_split", ptr(a), ptr(abias), ptr(gamma), ptr(sample_scale), ptr(mean),
          ptr(rstd), ptr(gx), ptr(gxb), rows, C, rps, ptr(gx0), ptr(ga), ptr(dgamma),
          ptr(dbeta), ptr(dabias), ptr(ws), ws_bytes, stream(), ctypes.c_void_p(fork[1].cuda_stream))
-    _wgrad_joined((ws, dgamma, dbeta, dabias))
+    _wgrad_joined((ws,), (dgamma, dbeta, dabias))
     return ga, dabias, gx0, dgamma, dbeta
 
 
@@ -1616,7 +1639,7 @@ def _merge_linear_bwd(ctx, xb, wb, ga):
         with torch.cuda.stream(fork[1]) if fork else contextlib.nullcontext():
             call("hvk_merge_weight_grad", ptr(ga), ptr(xb), ptr(dw), B, H, W, C, N, ptr(ws), nb, stream())
         if fork:
-            _wgrad_joined((ga, xb, dw, ws))
+            _wgrad_joined((ga, xb, ws), (dw,))
             _wgrad_outputs(dw)
     return gx, dw
 

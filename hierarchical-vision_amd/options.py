@@ -58,6 +58,11 @@ class HostOptions:
     # until RCCL over xGMI says otherwise (the dp2 gloo rehearsal measured -8 %); bench.py
     # --host-opt wgrad_stream_multi_rank=1 is the 8-GPU A/B, its `comm` block the diagnosis
     wgrad_stream_multi_rank: bool = False
+    # operands and workspaces of side-stream launches kept alive until the backward's join
+    # (ops.wgrad_hold) instead of freed with record_stream, whose blocks the caching allocator
+    # reuses only once the GPU has passed their last use: with the host steps ahead (SwinV2-B 384)
+    # every step mapped fresh HBM, 287 GB reserved and 470-650 ms per step
+    wgrad_hold: bool = True
     # clip + DecoupledSGDW (+ EMA) for every tensor in one fused launch set (hvk_sgdw_step)
     fused_optim: bool = True
     # windows 12 / 16 / 24: the forward keeps its log2 row constants for the backward

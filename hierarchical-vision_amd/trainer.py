@@ -106,6 +106,12 @@ class Trainer:
         self.grad_accum = resolve_grad_accum(grad_accum, dev)
         # a list -> each eager step appends its exchange timing events (comm_report); None: off
         self.comm_timing = None
+        # eager steps the host may have enqueued ahead of the GPU (None: unbounded, the default;
+        # bench.py --steps-in-flight).  The side stream's buffers no longer need it
+        # (ops.wgrad_hold), and bounding the SwinV2-T step to 2 cost 1.5 %
+        # (profiles/round6/inflight/).
+        self.max_steps_in_flight = None
+        self._in_flight = []
         self._run(Event.INIT)
 
     def _run(self, event):
@@ -115,6 +121,8 @@ class Trainer:
 
     def train_step(self, batch):
         st = self.state
+        if self.max_steps_in_flight and len(self._in_flight) >= self.max_steps_in_flight:
+            self._in_flight.pop(0).synchronize()  # the step max_steps_in_flight back is done
         if self.device_transforms is not None:
             batch = self.device_transforms(batch)
         # every .grad None and the arrival counts re-armed before the backward: after a
@@ -168,6 +176,10 @@ class Trainer:
         self.buckets.reset()
         st.timestamp_batch += 1
         self._run(Event.BATCH_END)
+        if self.max_steps_in_flight and batch[0].device.type == "cuda":
+            done = torch.cuda.Event()
+            done.record()
+            self._in_flight.append(done)
         return st.loss
 
     def _grad_mean(self, wait=True):
