@@ -198,9 +198,11 @@ def test_gemm_tile_sparse_pattern_pins_layout(N):
     assert torch.equal(y.float(), ref)
 
 
-def test_gemm_tile_gelu_matches_fp32():
+@pytest.mark.parametrize("M,K,N", [(50176, 384, 1536), (1000, 384, 1536), (1000, 512, 2048), (4096, 768, 3072)])
+def test_gemm_tile_gelu_matches_fp32(M, K, N):
+    """fc1 + bias + GELU on the tiled kernel (EPI 1; 128-column tiles stage h and GELU(h) as two
+    LDS images, HVK_EPI1_TWO), ragged M included, against fp32 math on the same bf16 operands."""
     from hvamd import _lib
-    M, K, N = 50176, 384, 1536
     g = torch.Generator(device="cuda").manual_seed(7)
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
