@@ -27,6 +27,10 @@
 #define HVK_FWD_ROWSUM_MFMA 1
 #endif
 
+#ifndef HVK_LARGE_TAB_EARLY  // 1: the forward reads all its tiles' bias C operands at each chunk's start
+#define HVK_LARGE_TAB_EARLY 1
+#endif
+
 namespace hvk_wmsa {
 namespace {
 
@@ -302,12 +306,23 @@ __global__ __launch_bounds__(64 * FCfg<WIN>::WAVES, FCfg<WIN>::MINW) void wmsa_f
         }
         const uint4 one = (K::N % 32 != 0 && c == K::NC - 1) ? one_last : one_full;
         (void)one;
+        // TAB_EARLY: every tile's bias C operands read with the chunk's K / V fragments, so their
+        // latency is not exposed in front of each tile's score MFMAs (+16 VGPRs)
+        hvk_f32x4 cb[HVK_LARGE_TAB_EARLY ? QT : 1][2];
+        if (HVK_LARGE_TAB_EARLY) {
+#pragma unroll
+          for (int j = 0; j < QT; ++j)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) cb[j][t] = lds_ld4f(tb[t] - 4u * (uint32_t)(F::DR * j));
+        }
 #pragma unroll
         for (int j = 0; j < QT; ++j) {
           hvk_f32x4 st[2];
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            st[t] = hvk_mfma16(kf[t], qf[j], lds_ld4f(tb[t] - 4u * (uint32_t)(F::DR * j)));
+            st[t] = hvk_mfma16(kf[t], qf[j],
+                               HVK_LARGE_TAB_EARLY ? cb[HVK_LARGE_TAB_EARLY ? j : 0][t]
+                                                   : lds_ld4f(tb[t] - 4u * (uint32_t)(F::DR * j)));
             if (EDGE) {
               const int qy = qy0 + (F::DQ / WIN) * j;
               const int band = ((int)((unsigned)(lim - 1 - qy) >> 31) & erow) |
