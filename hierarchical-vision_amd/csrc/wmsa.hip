@@ -704,10 +704,10 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 // Sum the (head, chunk) slots in chunk order into the CPB-table gradient [nH, R*R], d scale and
 // d q_bias, and leave the workspace zero for the next call.
 template <int WIN>
-__global__ __launch_bounds__(256) void wmsa_finalize_kernel(BwdArgs a, float* __restrict__ dtab,
+__global__ __launch_bounds__(FIN_THREADS) void wmsa_finalize_kernel(BwdArgs a, float* __restrict__ dtab,
                                                             float* __restrict__ dscale,
                                                             float* __restrict__ dqb) {
-  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x);
+  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x, blockIdx.y);
 }
 
 template <int WIN>
@@ -758,7 +758,7 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
     }
   }
   HVK_CHECK_LAUNCH("wmsa_bwd");
-  hipLaunchKernelGGL(wmsa_finalize_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dbias_table,
+  hipLaunchKernelGGL(wmsa_finalize_kernel<WIN>, dim3(a.g.nH, finalize_blocks_y(WIN)), dim3(FIN_THREADS), 0, st, a, dbias_table,
                      dscale, dqb);
   HVK_CHECK_LAUNCH("wmsa_finalize");
   return HVK_OK;

@@ -1060,10 +1060,10 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 
 // sum the (head, chunk) slots in chunk order into dtab / dscale / dq_bias, leave the workspace zero
 template <int WIN>
-__global__ __launch_bounds__(256) void wmsa_finalize_large_kernel(BwdArgs a, float* __restrict__ dtab,
+__global__ __launch_bounds__(FIN_THREADS) void wmsa_finalize_large_kernel(BwdArgs a, float* __restrict__ dtab,
                                                                   float* __restrict__ dscale,
                                                                   float* __restrict__ dqb) {
-  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x);
+  finalize_slots<WIN>(a, dtab, dscale, dqb, blockIdx.x, blockIdx.y);
 }
 
 template <int WIN, bool LSE>
@@ -1110,7 +1110,8 @@ int launch_bwd_large(const BwdArgs& a, float* dtab, float* dscale, float* dqb, h
   if (a.lse) launch_bwd_large_<WIN, true>(a, st);
   else launch_bwd_large_<WIN, false>(a, st);
   HVK_CHECK_LAUNCH("wmsa_bwd_large");
-  hipLaunchKernelGGL(wmsa_finalize_large_kernel<WIN>, dim3(a.g.nH), dim3(256), 0, st, a, dtab, dscale, dqb);
+  hipLaunchKernelGGL(wmsa_finalize_large_kernel<WIN>, dim3(a.g.nH, finalize_blocks_y(WIN)), dim3(FIN_THREADS), 0, st, a,
+                     dtab, dscale, dqb);
   HVK_CHECK_LAUNCH("wmsa_finalize_large");
   return HVK_OK;
 }
