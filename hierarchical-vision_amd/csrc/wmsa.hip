@@ -616,11 +616,6 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
     lds_barrier();  // phase B reads done: the images are free for the next window
     BSTAMP(6);
   }
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    hvk_bst16(r_dqkv, st_off[j], st_k[j]);
-    hvk_bst16(r_dqkv, st_off[j] + 2 * C, st_v[j]);
-  }
 #ifdef HVK_STAMPS
   if (lane == 0)
     for (int k = 0; k < 7; ++k) atomicAdd(&g_bwd_stamps[k], st_acc[k]);
@@ -637,7 +632,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
   static_assert(kThreads == 256, "four waves: two pairs");
   constexpr int RB = K::R * K::R, SLOT = bwd_slot_floats(WIN);
   static_assert(RB <= kThreads, "one bin per thread");
-  __syncthreads();
+  lds_barrier();  // LDS only: the last window's dQ / dK / dV stores stay in flight
   const float inv_scale = 1.f / scale;
   float* red = reinterpret_cast<float*>(img0) + pair * (PC::PAIR_LDS / 2);  // pair p's images
 #pragma unroll
@@ -649,28 +644,42 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       *reinterpret_cast<float4*>(red + ((qi * NT + ki) * 64 + lane) * 4) =
           make_float4(dbias[j][ki][0], dbias[j][ki][1], dbias[j][ki][2], dbias[j][ki][3]);
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: the last window's dQ / dK / dV stores stay in flight
   const float* red0 = reinterpret_cast<const float*>(img0);
   const int tid = threadIdx.x;
+#ifdef HVK_STAMPS
+  const unsigned long long st_fold0 = __builtin_amdgcn_s_memtime();
+#endif
   float binv = 0.f;
   if (tid < RB) {  // bin (dy, dx) = (q_y - k_y, q_x - k_x) + (w - 1)
     const int dy = tid / K::R - (WIN - 1), dx = tid % K::R - (WIN - 1);
     const int y0 = dy > 0 ? dy : 0, y1 = dy < 0 ? WIN + dy : WIN;
     const int x0 = dx > 0 ? dx : 0, x1 = dx < 0 ? WIN + dx : WIN;
-    for (int qy = y0; qy < y1; ++qy)
-      for (int qx = x0; qx < x1; ++qx) {
-        const int q = qy * WIN + qx, key = (qy - dy) * WIN + (qx - dx);
+    // every (q_y, q_x) of the window unrolled with a predicate (the same (q_y, q_x) order and
+    // additions as a loop over the bin's own range): the reads no longer wait one by one behind
+    // a divergent loop (the fold was 15-25 % of a stage-2/3 workgroup's life, HVK_STAMPS)
+#pragma unroll
+    for (int qy = 0; qy < WIN; ++qy)
+#pragma unroll
+      for (int qx = 0; qx < WIN; ++qx) {
+        const bool in = qy >= y0 && qy < y1 && qx >= x0 && qx < x1;
+        const int q = qy * WIN + qx, key = in ? (qy - dy) * WIN + (qx - dx) : 0;
         const int e = ((q >> 4) * NT + (key >> 4)) * 256 + ((q & 15) + 16 * ((key & 15) >> 2)) * 4 + (key & 3);
-        binv += red0[e] + red0[PC::PAIR_LDS / 2 + e];
+        const float t = red0[e] + red0[PC::PAIR_LDS / 2 + e];
+        binv = in ? binv + t : binv;
       }
   }
+#ifdef HVK_STAMPS
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const unsigned long long st_fold1 = __builtin_amdgcn_s_memtime();
+#endif
   dscale = hvk_wave_sum(dscale);
   float qbv[2][4];
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) qbv[dt][r] = hvk_row16_sum(dqb[dt][r]);
-  __syncthreads();  // the bin reads are done: stage the wave sums over the partials
+  lds_barrier();  // the bin reads are done: stage the wave sums over the partials
   float* stg = reinterpret_cast<float*>(img0);
   // NORMED: the products summed were dS (sc2 cos)
   if (lane == 0) stg[wave] = NORMED ? dscale * inv_scale * inv_sc2 : dscale * inv_scale;
@@ -680,7 +689,7 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) stg[8 + wave * 32 + 16 * dt + 4 * gq + r] = qbv[dt][r];
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: the last window's dQ / dK / dV stores stay in flight
   float* slot = a.dbias_acc + ((size_t)h * a.slot_stride + chunk) * SLOT;
   for (int i = tid; i < SLOT; i += kThreads) {
     float v;
@@ -690,13 +699,23 @@ __global__ __launch_bounds__(kThreads, 2) void wmsa_bwd_pair_kernel(BwdArgs a) {
       const int c = i - RB - 1;
       v = (stg[8 + c] + stg[40 + c]) + (stg[72 + c] + stg[104 + c]);
     }
-    slot[i] += v;
+    slot[i] = a.slot_add ? slot[i] + v : v;
+  }
+  // the last window's dK / dV leave here, after the fold: issued before it, their data registers
+  // could not be reused until the stores had read them, and the fold waited for them (vmcnt;
+  // 35-39 % of a stage-2/3 workgroup's teardown, HVK_STAMPS)
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) {
+    hvk_bst16(r_dqkv, st_off[j], st_k[j]);
+    hvk_bst16(r_dqkv, st_off[j] + 2 * C, st_v[j]);
   }
 #ifdef HVK_STAMPS
   __syncthreads();
   if (lane == 0) {
     atomicAdd(&g_bwd_stamps[8], st_acc_setup);
     atomicAdd(&g_bwd_stamps[9], __builtin_amdgcn_s_memtime() - st_loop_end);
+    atomicAdd(&g_bwd_stamps[10], st_fold0 - st_loop_end);  // stores issued, partials staged
+    atomicAdd(&g_bwd_stamps[11], st_fold1 - st_fold0);     // the bins fold
   }
 #endif
 }
@@ -739,6 +758,7 @@ int launch_bwd(const BwdArgs& a, float* dbias_table, float* dscale, float* dqb, 
     for (int b0 = 0; b0 < a.g.B; b0 += per) {
       BwdArgs s = a;
       s.g.B = a.g.B - b0 < per ? a.g.B - b0 : per;
+      s.slot_add = b0 > 0;
       s.g.n_windows = s.g.B * a.g.nWh * a.g.nWw;
       if (s.g.n_chunks > s.g.n_windows) s.g.n_chunks = s.g.n_windows;
       s.qkv += b0 * tok * 3 * a.g.C;

@@ -183,6 +183,8 @@ struct BwdArgs {
   // every parameter gradient is deterministic (no float atomics in any order)
   float* dbias_acc;          // [nH][slot_stride][bwd_slot_floats(win)]
   int slot_stride;           // slots per head (>= n_chunks of every launch over this workspace)
+  int slot_add;              // 0: the first launch over the workspace in this call stores its slots
+                             // (no load); 1: a later batch slice adds to them in stream order
   const float* rn;           // [T, 2nH] 1/max(||q||, eps), 1/max(||k||, eps) when q and k arrive
                              // normalised, q as q^ * scale * log2e (windows <= 8); null: raw q, k
   WmsaGeom g;

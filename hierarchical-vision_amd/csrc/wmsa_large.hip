@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
     float v = 0.f;
 #pragma unroll
     for (int c = 0; c < F::WAVES; ++c) v += bins[c * F::RRP + e];
-    slot[e] += v;
+    slot[e] = a.slot_add ? slot[e] + v : v;
   }
   dscale = hvk_wave_sum(dscale);
   float qbv[8];
@@ -1050,11 +1050,11 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
 #pragma unroll
     for (int e = 0; e < 8; ++e) stg[16 + wave * 32 + pcol + e] = qbv[e];
   }
-  __syncthreads();
+  lds_barrier();  // LDS only: the dK / dV and slot stores stay in flight
   if (threadIdx.x < 33) {
     float v = 0.f;
     for (int w = 0; w < F::WAVES; ++w) v += threadIdx.x == 0 ? stg[w] : stg[16 + w * 32 + threadIdx.x - 1];
-    slot[K::RR + threadIdx.x] += v;
+    slot[K::RR + threadIdx.x] = a.slot_add ? slot[K::RR + threadIdx.x] + v : v;
   }
 }
 

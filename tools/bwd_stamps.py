@@ -58,6 +58,9 @@ def main():
         print(f"  {p:40s} {buf[k] / waves:10.0f} cyc/wave  {100 * buf[k] / tot:5.1f} %")
     print(f"  setup (entry -> loop)                    {buf[8] / waves:10.0f} cyc/wave")
     print(f"  teardown (loop -> exit)                  {buf[9] / waves:10.0f} cyc/wave")
+    print(f"    partials staged in LDS                 {buf[10] / waves:10.0f} cyc/wave")
+    print(f"    bins fold                              {buf[11] / waves:10.0f} cyc/wave")
+    print(f"    wave sums, slot add, stores drained    {(buf[9] - buf[10] - buf[11]) / waves:10.0f} cyc/wave")
 
 
 if __name__ == "__main__":
