@@ -169,10 +169,22 @@ __device__ void build_bounded_table(float* tab, float* wmax, const float* __rest
     const int qi = blk / K::NT, ki = blk % K::NT;
     const int q = 16 * qi + (lane & 15), key = 16 * ki + 4 * (lane >> 4) + r;
     real[k] = q < K::N && key < K::N;
-    v[k] = key >= K::N ? -INFINITY : 0.f;
+    // every load unconditional (a padding entry reads entry 0 and discards it): behind a branch
+    // each of the PER loads waited for itself, PER global-load latencies per workgroup setup
+    const int si = real[k] ? (q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1) : 0;
+    v[k] = src[si];
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    const int r = e & 3, lane = (e >> 2) & 63, blk = e >> 8;
+    const int ki = blk % K::NT;
+    const int key = 16 * ki + 4 * (lane >> 4) + r;
     if (real[k]) {
-      v[k] = src[(q / WIN - key / WIN + WIN - 1) * K::R + (q % WIN - key % WIN + WIN - 1)] * HVK_LOG2E;
+      v[k] *= HVK_LOG2E;
       mx = fmaxf(mx, v[k]);
+    } else {
+      v[k] = key >= K::N ? -INFINITY : 0.f;
     }
   }
   mx = wave_max(mx);
