@@ -888,7 +888,10 @@ int wmsa_bwd(const void* qkv, const float* rn, const void* dout, const void* out
   // the rounding left 64 CUs idle), the (chunk, head) items dealt to the XCDs in runs of at
   // most 32 (one resident workgroup per CU of each XCD)
   {
-    int c = 512 / num_heads;  // two resident workgroups per CU
+#ifndef HVK_BWD_SLOTS  // workgroups per launch the chunk count aims at (A/B build switch)
+#define HVK_BWD_SLOTS 512
+#endif
+    int c = HVK_BWD_SLOTS / num_heads;  // two resident workgroups per CU
     if (c < 1) c = 1;
     a.g.n_chunks = c < a.g.n_windows ? c : a.g.n_windows;
     a.g.xcd_runs = 1;
