@@ -27,6 +27,9 @@
 #define HVK_FWD_ROWSUM_MFMA 1
 #endif
 
+#ifndef HVK_LARGE_OPS_EARLY  // 1: the backward's phase 1 reads a chunk's operands before its MFMAs
+#define HVK_LARGE_OPS_EARLY 1
+#endif
 #ifndef HVK_LARGE_TAB_EARLY  // 1: the forward reads all its tiles' bias C operands at each chunk's start
 #define HVK_LARGE_TAB_EARLY 1
 #endif
@@ -741,13 +744,21 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       float rnq;
       const uint4 qs = l2_normalize_seq(cur.q, rnq, sc2);
       float rowc, delta;  // row constant (rel. to M_h) and delta for dS
-      // S' (masked) and dP - d0 of (chunk c, half t): d0 (the row's delta, or 0) enters the dP
-      // MFMA as its C operand
-      auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d, float d0) {
-        constexpr bool EDGE = decltype(edge_t)::value;
+      // a chunk half's operands: k^ / v fragments and the lane's 4 bias entries (C operand)
+      struct TOps {
+        uint4 a0, a1;
+        hvk_f32x4 cb;
+      };
+      auto tile_ops = [&](int c, int t, int ky, int kx) {
         const float* tp = mtab + (tq + ky * K::R + kx);
-        s = hvk_mfma16(lds16(img0, fm16(32 * c + 16 * t + li, gq)), qs, hvk_f32x4{tp[0], tp[1], tp[2], tp[3]});
-        d = hvk_mfma16(lds16(img1, fm16(32 * c + 16 * t + li, gq)), cur.dof, hvk_f32x4{-d0, -d0, -d0, -d0});
+        return TOps{lds16(img0, fm16(32 * c + 16 * t + li, gq)), lds16(img1, fm16(32 * c + 16 * t + li, gq)),
+                    hvk_f32x4{tp[0], tp[1], tp[2], tp[3]}};
+      };
+      auto tile_from = [&](auto edge_t, int c, int t, int ky, int kx, const TOps& o, hvk_f32x4& s, hvk_f32x4& d,
+                           float d0) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        s = hvk_mfma16(o.a0, qs, o.cb);
+        d = hvk_mfma16(o.a1, cur.dof, hvk_f32x4{-d0, -d0, -d0, -d0});
         if (EDGE) {
           const bool rmis = edge_r && ((ky >= lim) != (qy >= lim));
 #pragma unroll
@@ -762,6 +773,11 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
           for (int r = 0; r < 4; ++r)
             if (kp + r >= K::N) s[r] = -INFINITY;
         }
+      };
+      // S' (masked) and dP - d0 of (chunk c, half t): d0 (the row's delta, or 0) enters the dP
+      // MFMA as its C operand
+      auto tile = [&](auto edge_t, int c, int t, int ky, int kx, hvk_f32x4& s, hvk_f32x4& d, float d0) {
+        tile_from(edge_t, c, t, ky, kx, tile_ops(c, t, ky, kx), s, d, d0);
       };
       if (LSE) {
         rowc = cur.lse - Mh;
@@ -839,10 +855,21 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
       auto loopB = [&](auto edge_t) {
         for_chunks([&](int c, const int (&ky)[2], const int (&kx)[2]) {
           float p[8], ds[8];
+          // OPS_EARLY: both halves' operands and the transposed k^ fragments of dQ read up front,
+          // one LDS wait per chunk instead of one in front of every MFMA
+          TOps o[2];
+          uint4 kt[2];
+          if (HVK_LARGE_OPS_EARLY) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) o[t] = tile_ops(c, t, ky[t], kx[t]);
+            kt[0] = tr_frag(img0, c, 0, li, gq);
+            kt[1] = tr_frag(img0, c, 1, li, gq);
+          }
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
             hvk_f32x4 s, d;
-            tile(edge_t, c, t, ky[t], kx[t], s, d, delta);  // d = dP - delta
+            if (HVK_LARGE_OPS_EARLY) tile_from(edge_t, c, t, ky[t], kx[t], o[t], s, d, delta);  // d = dP - delta
+            else tile(edge_t, c, t, ky[t], kx[t], s, d, delta);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               p[4 * t + r] = __builtin_amdgcn_exp2f(s[r] - rowc);  // padding keys: 0
@@ -852,7 +879,8 @@ __global__ __launch_bounds__(64 * BCfg<WIN>::WAVES, 2) void wmsa_bwd_large_kerne
           }
           const uint4 dsf = make_uint4(hvk_pack2(ds[0], ds[1]), hvk_pack2(ds[2], ds[3]),
                                        hvk_pack2(ds[4], ds[5]), hvk_pack2(ds[6], ds[7]));
-          const uint4 kf0 = tr_frag(img0, c, 0, li, gq), kf1 = tr_frag(img0, c, 1, li, gq);
+          const uint4 kf0 = HVK_LARGE_OPS_EARLY ? kt[0] : tr_frag(img0, c, 0, li, gq);
+          const uint4 kf1 = HVK_LARGE_OPS_EARLY ? kt[1] : tr_frag(img0, c, 1, li, gq);
           dq[0] = hvk_mfma16(kf0, dsf, dq[0]);
           dq[1] = hvk_mfma16(kf1, dsf, dq[1]);
           if (LSE) {
