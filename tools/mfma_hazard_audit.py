@@ -66,6 +66,42 @@ def states(mn, ops):
     return 1
 
 
+SREG = re.compile(r"^s\[(\d+):(\d+)\]$|^s(\d+)$")
+
+
+def sregs(op):
+    m = SREG.match(op)
+    if not m:
+        return set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def branch_facts(mn, f, known, vcc):
+    """Path facts for the structurizer's flag idiom (`s_mov_b64 sX, 0 / -1` on one arm, then
+    `s_andn2_b64 vcc, exec, sX` + `s_cbranch_vccnz`): -> (known, vcc, only) where known maps an
+    SGPR pair to the constant this path last wrote to it, vcc is "nz" / "z" / None (unknown), and
+    only is "taken" / "fall" when this is a branch whose direction the path fixes.  exec is taken
+    as non-zero: with exec = 0 no vector write happens, so no hazard is lost."""
+    dst = f[0] if f else ""
+    if mn.startswith("s_") and not mn.startswith(("s_cbranch", "s_branch", "s_waitcnt", "s_nop")):
+        w = sregs(dst)  # any scalar write forgets the pairs it overlaps
+        known = {k: v for k, v in known.items() if not (sregs(k) & w)}
+    if mn == "s_mov_b64" and SREG.match(dst) and f[1:2] in (["0"], ["-1"]):
+        return {**known, dst: int(f[1])}, vcc, None
+    if mn in ("s_andn2_b64", "s_and_b64") and f[:2] == ["vcc", "exec"] and len(f) == 3 and f[2] in known:
+        zero = known[f[2]] == (0 if mn == "s_and_b64" else -1)
+        return known, ("z" if zero else "nz"), None
+    if mn in ("s_cbranch_vccnz", "s_cbranch_vccz"):
+        if vcc is None:
+            return known, vcc, None
+        return known, vcc, "taken" if (vcc == "nz") == (mn == "s_cbranch_vccnz") else "fall"
+    if "vcc" in f or mn.startswith("v_cmp"):  # anything else that may write vcc
+        vcc = None
+    return known, vcc, None
+
+
 def audit(lines, labels, min_states):
     bad = []
     for i, (mn, ops) in enumerate(lines):
@@ -73,15 +109,17 @@ def audit(lines, labels, min_states):
             continue
         fields = [f.strip() for f in ops.split(",")]
         seen = set()
-        work = [(i + 1, 0, frozenset(regs(fields[0])))]
+        work = [(i + 1, 0, frozenset(regs(fields[0])), {}, None)]
         while work:
-            j, st, dst = work.pop()
+            j, st, dst, known, vcc = work.pop()
             while j < len(lines) and st < min_states and dst:
-                if (j, st, dst) in seen:
+                key = (j, st, dst, frozenset(known.items()), vcc)
+                if key in seen:
                     break
-                seen.add((j, st, dst))
+                seen.add(key)
                 m2, o2 = lines[j]
                 f2 = [f.strip() for f in o2.split(",")]
+                known, vcc, only = branch_facts(m2, f2, known, vcc)
                 touched = regs(o2) & dst
                 if touched:
                     is_mfma = m2.startswith("v_mfma") and len(f2) >= 4
@@ -101,9 +139,9 @@ def audit(lines, labels, min_states):
                     break
                 if m2.startswith("s_cbranch") or m2 == "s_branch":
                     tgt = labels.get(o2.strip())
-                    if tgt is not None:
-                        work.append((tgt, st + 1, dst))
-                    if m2 == "s_branch":
+                    if tgt is not None and only != "fall":
+                        work.append((tgt, st + 1, dst, known, vcc))
+                    if m2 == "s_branch" or only == "taken":
                         break
                 st += states(m2, o2)
                 j += 1
