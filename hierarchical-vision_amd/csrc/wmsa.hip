@@ -888,11 +888,9 @@ int wmsa_bwd(const void* qkv, const float* rn, const void* dout, const void* out
   // the rounding left 64 CUs idle), the (chunk, head) items dealt to the XCDs in runs of at
   // most 32 (one resident workgroup per CU of each XCD)
   {
-#ifndef HVK_BWD_SLOTS  // workgroups per launch the chunk count aims at (A/B build switch)
-#define HVK_BWD_SLOTS 512
-#endif
-    int c = HVK_BWD_SLOTS / num_heads;  // two resident workgroups per CU
-    if (c < 1) c = 1;
+    // HVK_BWD_SLOTS / nH chunks (two resident workgroups per CU): the workspace's slots per head,
+    // so the chunk count and the workspace size come from one place
+    const int c = hvk_wmsa::bwd_slot_stride(num_heads, false);
     a.g.n_chunks = c < a.g.n_windows ? c : a.g.n_windows;
     a.g.xcd_runs = 1;
   }

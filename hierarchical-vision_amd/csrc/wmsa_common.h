@@ -230,13 +230,17 @@ int win_fwd(FwdArgs& a, int B, int H, int W, int C, int nH, int win, int shift, 
 __host__ __device__ constexpr int bwd_slot_floats(int win) { return (2 * win - 1) * (2 * win - 1) + 33; }
 // slots per head: the most chunks a launch over nH heads uses (wmsa_bwd: 512 / nH for windows
 // <= 8, make_geom's 256-workgroup plan for the large windows)
+#ifndef HVK_BWD_SLOTS  // w <= 8 backward: workgroups per launch the chunk count aims at (A/B build switch)
+#define HVK_BWD_SLOTS 512
+#endif
+// slots per head of the backward workspace = the chunk count of the w <= 8 launch (at most)
 inline int bwd_slot_stride(int num_heads, bool large) {
   if (num_heads <= 0) return 1;
   if (large) {
     const int c = 256 / num_heads / 8 * 8;
     return c < 8 ? 8 : c;
   }
-  const int c = 512 / num_heads;
+  const int c = HVK_BWD_SLOTS / num_heads;
   return c < 1 ? 1 : c;
 }
 
