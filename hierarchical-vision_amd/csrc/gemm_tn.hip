@@ -283,7 +283,7 @@ __global__ __launch_bounds__(32 * NPH) void dw_reduce_kernel(const float4* __res
 // with the fused bias gradient on every stage 1-3 shape); B256 / B128: 128 x 256 and 128 x 128
 // tiles for the widths 192 does not divide (SwinV2-B: C = 128 ... 1024)
 // V_T4 .. V_T8C are the option "dw_tile" values 4 .. 8 (tile_variant): keep their numbers
-enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C, V_B256, V_B128, V_96x48 };
+enum { V_288x96, V_96x96, V_384x96, V_96x384, V_T4, V_T8A, V_T8B, V_T8W, V_T8C, V_B256, V_B128, V_96x48, V_128x48 };
 static_assert(V_T4 == 4 && V_T8C == 8, "dw_tile option values");
 
 struct Plan {
@@ -302,6 +302,7 @@ bool plan(int M, int N, int K, Plan& p) {
   else if (N == 384 && K == 96) p.var = V_384x96, p.tk = 96, p.tn = 384;
   else if (N == 96 && K == 384) p.var = V_96x384, p.tk = 384, p.tn = 96;
   else if (N == 96 && K == 48) p.var = V_96x48, p.tk = 48, p.tn = 96;  // the patch embedding (4x4x3 -> 96)
+  else if (N == 128 && K == 48) p.var = V_128x48, p.tk = 48, p.tn = 128;  // SwinV2-B's (4x4x3 -> 128)
   else if (N % 192 == 0 && K % 192 == 0 && N <= 8192 && K <= 8192) {
     p.var = tile_variant();
     if (p.var < V_T4 || p.var > V_T8C || (p.var == V_T8W && N % 384)) p.var = V_T4;
@@ -402,6 +403,7 @@ static int weight_grad(const void* g, const void* x, float* dw, float* db, int M
     case V_288x96: rc = launch<3, 9, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x96: rc = launch<3, 3, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x48: rc = launch<3, 3, 1, 2>(gb, xb, P, wd, N, K, p, st); break;
+    case V_128x48: rc = launch<3, 4, 1, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_384x96: rc = launch<3, 12, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_96x384: rc = launch<12, 3, 2, 2>(gb, xb, P, wd, N, K, p, st); break;
     case V_T8A: rc = launch<6, 3, 2, 4>(gb, xb, P, wd, N, K, p, st); break;

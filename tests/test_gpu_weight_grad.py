@@ -11,7 +11,7 @@ CASES = [(288, 96, 32 * 517), (96, 96, 6272), (384, 96, 12544), (96, 384, 12544)
          (576, 192, 3136), (192, 192, 800), (768, 192, 3136), (192, 768, 3136),
          (1152, 384, 1568), (384, 384, 1568), (1536, 384, 1568), (384, 1536, 1568),
          (2304, 768, 12544), (768, 3072, 2048), (192, 384, 6272), (384, 768, 1568), (32 * 6, 192, 32),
-         (96, 48, 32 * 999)]
+         (96, 48, 32 * 999), (128, 48, 32 * 999), (128, 48, 32 * 4608)]
 
 
 def _ref(g, x):
